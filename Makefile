@@ -1,0 +1,48 @@
+# Top-level build (GNU make; no cmake/ninja needed).
+#
+#   make            libvp8host.so (C11 front end), libvp8g.so (HIP gfx950 kernels + C-ABI shim),
+#                   bin/decoder (the CLI), oracle/liboracle.so (+ oracle/_ref when the reference exists)
+#   make lib        just the product libraries + CLI
+#
+# Everything is built in-tree so the .so files travel to the GPU box with the snapshot.
+
+PKG := webp-decoder_amd
+LIB := $(PKG)/lib
+BIN := $(PKG)/bin
+HIPCC ?= /opt/rocm/bin/hipcc
+CC ?= gcc
+OFFLOAD_ARCH ?= gfx950
+
+HOST_SRC := $(PKG)/host/webp_riff.c $(PKG)/host/vp8_parse.c $(PKG)/host/vp8_synth.c
+HOST_HDR := $(PKG)/host/vp8_front.h $(PKG)/host/vp8_bool.h $(PKG)/host/vp8_tables.inc include/vp8g.h
+HIP_SRC := $(PKG)/csrc/vp8g_kernels.hip $(PKG)/csrc/vp8g_shim.hip
+HIP_HDR := $(PKG)/csrc/vp8g_device.h include/vp8g.h
+
+CFLAGS := -std=c11 -O3 -march=x86-64-v3 -Wall -Wextra -Wpedantic -fPIC -D_POSIX_C_SOURCE=200809L
+HIPFLAGS := -std=c++17 -O3 --offload-arch=$(OFFLOAD_ARCH) -fPIC -Wall -Wno-unused-function \
+	-fvisibility=hidden -I include -munsafe-fp-atomics
+
+all: lib oracle
+
+lib: $(LIB)/libvp8host.so $(LIB)/libvp8g.so $(BIN)/decoder
+
+$(LIB) $(BIN):
+	mkdir -p $@
+
+$(LIB)/libvp8host.so: $(HOST_SRC) $(HOST_HDR) | $(LIB)
+	$(CC) $(CFLAGS) -shared -Wl,-Bsymbolic -o $@ $(HOST_SRC)
+
+$(LIB)/libvp8g.so: $(HIP_SRC) $(HIP_HDR) | $(LIB)
+	$(HIPCC) $(HIPFLAGS) -shared -Wl,-Bsymbolic -o $@ $(HIP_SRC) -lpthread
+
+$(BIN)/decoder: $(PKG)/host/decoder_main.c $(LIB)/libvp8host.so $(LIB)/libvp8g.so | $(BIN)
+	$(CC) $(CFLAGS) -o $@ $(PKG)/host/decoder_main.c -L$(LIB) -lvp8host -lvp8g -Wl,-rpath,'$$ORIGIN/../lib'
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf $(LIB) $(BIN)
+	$(MAKE) -C oracle clean
+
+.PHONY: all lib oracle clean

@@ -1,0 +1,221 @@
+/*
+ * vp8g.h -- C ABI of the MI355X-native VP8 keyframe reconstruction + loop-filter path.
+ *
+ * This header is the drop-in boundary.  The first half re-declares, layout-identically, the
+ * reference decoder's types and the five entry points of its m06/m07 hot path, so the
+ * reference's own callers (src/main.c:591, :665, :742, :811, :881; src/main_ultra.c:43)
+ * link against libvp8g.so unchanged.  The second half is an additive batch API used by the
+ * batch/multi-GPU driver and the benchmark (device-resident frames, one launch per batch).
+ *
+ * Plain C: no HIP or torch types appear in any signature.  Streams are passed as void*.
+ */
+#ifndef VP8G_H
+#define VP8G_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- Reference types (layout-identical) ------------------------------------------------ */
+
+/* reference: src/common/os.h:6-9 */
+#ifndef VP8G_NO_BYTESPAN
+typedef struct {
+	const uint8_t* data;
+	size_t size;
+} ByteSpan;
+#endif
+
+/* reference: src/m02_vp8_header/vp8_header.h:7-18 (28 bytes; width @20, height @22) */
+typedef struct {
+	int is_key_frame;
+	uint8_t profile;
+	int show_frame;
+	uint32_t first_partition_len;
+	int start_code_ok;
+	uint16_t width;
+	uint16_t height;
+	uint8_t x_scale;
+	uint8_t y_scale;
+} Vp8KeyFrameHeader;
+
+/* reference: src/m05_tokens/vp8_tokens.h:7-50 (200 bytes) */
+typedef struct {
+	uint32_t mb_cols;
+	uint32_t mb_rows;
+	uint32_t mb_total;
+	uint32_t part0_size_bytes;
+	uint32_t part0_bytes_used;
+	uint8_t part0_overread;
+	uint32_t part0_overread_bytes;
+	uint32_t token_part_size_bytes;
+	uint32_t token_part_bytes_used;
+	uint8_t token_overread;
+	uint32_t token_overread_bytes;
+	uint32_t token_overread_mb_index;
+	uint32_t token_overread_plane;
+	uint32_t token_overread_block_index;
+	uint32_t token_overread_coeff_i;
+	uint32_t token_overread_stage;
+	uint32_t mb_skip_coeff;
+	uint32_t mb_b_pred;
+	uint32_t ymode_counts[5];
+	uint32_t uv_mode_counts[4];
+	uint32_t bmode_counts[10];
+	uint32_t blocks_total_y2;
+	uint32_t blocks_total_y;
+	uint32_t blocks_total_u;
+	uint32_t blocks_total_v;
+	uint32_t blocks_nonzero_y2;
+	uint32_t blocks_nonzero_y;
+	uint32_t blocks_nonzero_u;
+	uint32_t blocks_nonzero_v;
+	uint32_t coeff_nonzero_total;
+	uint32_t coeff_eob_tokens;
+	uint32_t coeff_abs_max;
+	uint64_t coeff_hash_fnv1a64;
+} Vp8CoeffStats;
+
+/* reference: src/m05_tokens/vp8_tokens.h:52-99 (320 bytes).  The hot path's input:
+ * per-MB modes + dense int16 coefficients in natural (de-zigzagged) order. */
+typedef struct {
+	uint32_t mb_cols;
+	uint32_t mb_rows;
+	uint32_t mb_total;
+	uint8_t q_index;
+	int8_t y1_dc_delta_q;
+	int8_t y2_dc_delta_q;
+	int8_t y2_ac_delta_q;
+	int8_t uv_dc_delta_q;
+	int8_t uv_ac_delta_q;
+	uint8_t segmentation_enabled;
+	uint8_t segmentation_abs;
+	int8_t seg_quant_idx[4];
+	int8_t seg_lf_level[4];
+	uint8_t lf_use_simple;
+	uint8_t lf_level;
+	uint8_t lf_sharpness;
+	uint8_t lf_delta_enabled;
+	int8_t lf_ref_delta[4];
+	int8_t lf_mode_delta[4];
+	uint8_t* segment_id; /* [mb_total] 0..3 */
+	uint8_t* skip_coeff; /* [mb_total] */
+	uint8_t* has_coeff;  /* [mb_total] (may be NULL: treated as all zero) */
+	uint8_t* ymode;      /* [mb_total] 0..4 = DC,V,H,TM,B_PRED */
+	uint8_t* uv_mode;    /* [mb_total] 0..3 */
+	uint8_t* bmode;      /* [mb_total*16] 0..9 */
+	int16_t* coeff_y2;   /* [mb_total*16] */
+	int16_t* coeff_y;    /* [mb_total*256] */
+	int16_t* coeff_u;    /* [mb_total*64] */
+	int16_t* coeff_v;    /* [mb_total*64] */
+	Vp8CoeffStats stats;
+} Vp8DecodedFrame;
+
+/* reference: src/m06_recon/vp8_recon.h:10-18 (40 bytes). Planes are malloc()ed host memory. */
+typedef struct {
+	uint32_t width;
+	uint32_t height;
+	uint32_t stride_y;
+	uint32_t stride_uv;
+	uint8_t* y;
+	uint8_t* u;
+	uint8_t* v;
+} Yuv420Image;
+
+/* ---- Reference entry points (exact signatures) ----------------------------------------- */
+
+/* replaces src/m06_recon/vp8_recon.c:360 (decl vp8_recon.h:20).  Y zeroed, U/V = 128;
+ * stride_y = width, stride_uv = (width+1)/2.  0 / -1 + errno (EINVAL, ENOMEM). */
+int yuv420_alloc(Yuv420Image* img, uint32_t width, uint32_t height);
+
+/* replaces src/m06_recon/vp8_recon.c:387 (decl vp8_recon.h:21).  Plain free() of the planes. */
+void yuv420_free(Yuv420Image* img);
+
+/* replaces src/m06_recon/vp8_recon.c:714 (decl vp8_recon.h:25): recon only (decoder -yuv). */
+int vp8_reconstruct_keyframe_yuv(const Vp8KeyFrameHeader* kf, const Vp8DecodedFrame* decoded, Yuv420Image* out);
+
+/* replaces src/m06_recon/vp8_recon.c:718 (decl vp8_recon.h:28): recon + loop filter (-yuvf). */
+int vp8_reconstruct_keyframe_yuv_filtered(const Vp8KeyFrameHeader* kf, const Vp8DecodedFrame* decoded,
+                                          Yuv420Image* out);
+
+/* replaces src/m07_loopfilter/vp8_loopfilter.c:201 (decl vp8_loopfilter.h:14): in-place filter of a
+ * macroblock-aligned frame (width == mb_cols*16, height == mb_rows*16, else EINVAL). */
+int vp8_loopfilter_apply_keyframe(Yuv420Image* padded_img, const Vp8DecodedFrame* decoded);
+
+/* ---- Batch API (build-only, additive) --------------------------------------------------- */
+
+/* Per-frame launch descriptor (host computes it once per frame: geometry, output placement,
+ * dequant factors per segment (RFC 6386 14.1, reference vp8_recon.c:57-76) and loop-filter
+ * parameters per (segment, is_B_PRED) (reference vp8_loopfilter.c:166-199)). 176 bytes. */
+typedef struct {
+	uint32_t mb_cols, mb_rows;
+	uint32_t width, height;       /* crop (visible) size written to the output */
+	uint32_t stride_y, stride_uv; /* output strides in bytes */
+	uint64_t mb_offset;           /* index of this frame's first MB in the batch SoA arrays */
+	uint64_t out_y, out_u, out_v; /* byte offsets of the three planes in the output buffer */
+	uint64_t src_y, src_u, src_v; /* (loop-filter-only mode) byte offsets of the padded input */
+	uint32_t flags;               /* VP8G_F_* */
+	uint32_t src_stride_y, src_stride_uv;
+	uint32_t reserved;
+	int16_t dq[4][6];  /* [segment][Y1dc, Y1ac, UVdc, UVac, Y2dc, Y2ac] */
+	uint8_t lf[4][2][4]; /* [segment][is_bpred] = {level(E), interior I, hev T, 0}; level 0 = skip */
+} Vp8gFrameDesc;
+
+#define VP8G_F_LOOPFILTER 1u /* apply m07 (some MB has a non-zero level) */
+#define VP8G_F_SIMPLE 2u     /* simple filter (luma only) instead of normal */
+#define VP8G_F_LF_ONLY 4u    /* loop-filter-only: pixels come from src_* instead of recon */
+
+/* Device pointers of a batch, concatenated over frames in the exact per-array layout of
+ * Vp8DecodedFrame (so a frame uploads with nine plain memcpys).  MB index m of frame f is
+ * desc.mb_offset + m. */
+typedef struct {
+	const int16_t* coeff_y;  /* [MB*256] */
+	const int16_t* coeff_u;  /* [MB*64] */
+	const int16_t* coeff_v;  /* [MB*64] */
+	const int16_t* coeff_y2; /* [MB*16] */
+	const uint8_t* ymode;    /* [MB] */
+	const uint8_t* uv_mode;  /* [MB] */
+	const uint8_t* segment_id; /* [MB] */
+	const uint8_t* has_coeff;  /* [MB] */
+	const uint8_t* bmode;      /* [MB*16] */
+	const uint8_t* src;        /* LF-only mode input pixels (else NULL) */
+	uint32_t* status;          /* device word: 0 ok, else VP8G_ERR_* (kernel-detected) */
+} Vp8gBatchArrays;
+
+#define VP8G_ERR_TIMEOUT 1u /* a wavefront dependency wait exceeded its bound */
+
+/* Fill a descriptor for one frame.  kf may be NULL in LF-only mode.  Returns 0 / -1+errno. */
+int vp8g_make_frame_desc(const Vp8KeyFrameHeader* kf, const Vp8DecodedFrame* decoded, int filtered,
+                         uint64_t mb_offset, uint64_t out_offset, Vp8gFrameDesc* out);
+
+/* Bytes of cropped I420 output for a w x h frame (Y + 2 * ceil(w/2)*ceil(h/2)). */
+uint64_t vp8g_i420_size(uint32_t width, uint32_t height);
+
+/* Launch the fused recon(+LF) kernel over n frames on `hip_stream` (NULL = default stream).
+ * h_descs: host copy (launch geometry); d_descs: the same array in device memory.
+ * All pointers in `arrays` and d_out are device pointers.  Asynchronous; returns 0 or -1+errno.
+ * `waves_per_frame` 0 = default. */
+int vp8g_decode_batch_device(const Vp8gFrameDesc* h_descs, const Vp8gFrameDesc* d_descs, uint32_t n_frames,
+                             const Vp8gBatchArrays* arrays, uint8_t* d_out, void* hip_stream,
+                             uint32_t waves_per_frame);
+
+/* Host-side batch: upload n decoded frames, run one launch, download into n freshly
+ * yuv420_alloc()ed images.  Returns 0 / -1+errno (EIO on a HIP failure). */
+int vp8g_reconstruct_batch(const Vp8KeyFrameHeader* const* kfs, const Vp8DecodedFrame* const* frames, uint32_t n,
+                           int filtered, Yuv420Image* outs);
+
+/* Name of the last HIP error seen by this library in the calling thread ("" if none). */
+const char* vp8g_last_error(void);
+
+/* ABI version of this header (bumped on any layout change). */
+#define VP8G_ABI_VERSION 1
+uint32_t vp8g_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VP8G_H */

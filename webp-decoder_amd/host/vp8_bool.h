@@ -1,0 +1,106 @@
+/*
+ * vp8_bool.h -- RFC 6386 section 7 boolean entropy decoder (host, C11).
+ *
+ * Formulation: `value` is a window over the partition bits; the arithmetic-coder comparison
+ * is done against its top bits, `(value >> bits) >= split`, where `bits` counts the stream
+ * bits already loaded below the 8-bit comparison position.  Bytes past the end of the
+ * partition read as zero (same as reference bool_decoder.c:5-15).
+ *
+ * The reference loads 2 bytes at init and then one byte every time 8 normalisation shifts
+ * have accumulated (bool_decoder.c:17-39, :59-68).  We keep the total shift count `shifts`
+ * so its diagnostic counters (bytes used / overread bytes, reported by `decoder -info`) can
+ * be reproduced exactly without mimicking its byte-by-byte refill schedule.
+ */
+#ifndef VP8_BOOL_H
+#define VP8_BOOL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+typedef struct {
+	const uint8_t* next; /* next unread byte */
+	const uint8_t* end;
+	uint64_t value;
+	int bits;        /* bits below the comparison window */
+	uint32_t range;  /* 128..255 between calls */
+	uint64_t shifts; /* total normalisation shifts so far */
+	size_t size;     /* partition size in bytes */
+} Vp8Bool;
+
+static inline void vp8b_fill(Vp8Bool* b) {
+	while (b->bits <= 48) {
+		uint64_t byte = 0;
+		if (b->next < b->end) byte = *b->next++;
+		/* past the end: shift in zeros (the coder's defined padding) */
+		b->value = (b->value << 8) | byte;
+		b->bits += 8;
+	}
+}
+
+static inline void vp8b_init(Vp8Bool* b, const uint8_t* data, size_t size) {
+	b->next = data;
+	b->end = data + size;
+	b->value = 0;
+	b->bits = -8;
+	b->range = 255;
+	b->shifts = 0;
+	b->size = size;
+	vp8b_fill(b);
+}
+
+static inline int vp8b_read(Vp8Bool* b, uint32_t prob) {
+	uint32_t split = 1u + (((b->range - 1u) * prob) >> 8);
+	int bit;
+	if ((uint32_t)(b->value >> b->bits) >= split) {
+		b->value -= (uint64_t)split << b->bits;
+		b->range -= split;
+		bit = 1;
+	} else {
+		b->range = split;
+		bit = 0;
+	}
+	/* normalise: range back into [128, 255] */
+	int sh = __builtin_clz(b->range) - 24;
+	b->range <<= sh;
+	b->bits -= sh;
+	b->shifts += (uint64_t)sh;
+	if (b->bits < 0) vp8b_fill(b);
+	return bit;
+}
+
+static inline uint32_t vp8b_literal(Vp8Bool* b, int n) {
+	uint32_t v = 0;
+	while (n-- > 0) v = (v << 1) | (uint32_t)vp8b_read(b, 128);
+	return v;
+}
+
+/* magnitude then sign (RFC 6386 9.3 / 9.6 signed fields) */
+static inline int32_t vp8b_signed(Vp8Bool* b, int n) {
+	int32_t m = (int32_t)vp8b_literal(b, n);
+	if (m == 0) return 0;
+	return vp8b_read(b, 128) ? -m : m;
+}
+
+/* Tree decode: tree[] holds pairs of (left, right); entries <= 0 are leaves (-symbol). */
+static inline int vp8b_tree(Vp8Bool* b, const int8_t* tree, const uint8_t* probs, int node) {
+	for (;;) {
+		int next = tree[node + vp8b_read(b, probs[node >> 1])];
+		if (next <= 0) return -next;
+		node = next;
+	}
+}
+
+/* ---- reference-compatible diagnostics (see header comment) ---- */
+static inline uint64_t vp8b_ref_loads(const Vp8Bool* b) { return b->shifts >> 3; }
+static inline size_t vp8b_ref_init_bytes(const Vp8Bool* b) { return b->size < 2 ? b->size : 2; }
+static inline uint32_t vp8b_ref_overread_bytes(const Vp8Bool* b) {
+	uint64_t avail = b->size - vp8b_ref_init_bytes(b);
+	uint64_t loads = vp8b_ref_loads(b);
+	return loads > avail ? (uint32_t)(loads - avail) : 0u;
+}
+static inline size_t vp8b_ref_bytes_used(const Vp8Bool* b) {
+	uint64_t used = vp8b_ref_init_bytes(b) + vp8b_ref_loads(b);
+	return used > b->size ? b->size : (size_t)used;
+}
+
+#endif

@@ -1,0 +1,409 @@
+/*
+ * vp8_parse.c -- key-frame header remainder, per-macroblock modes and coefficient tokens
+ * (RFC 6386 sections 9, 11, 13), producing the reference's Vp8DecodedFrame.
+ *
+ * Output semantics follow the reference m05 (src/m05_tokens/vp8_tokens.c) exactly, because the
+ * hot path's parity is defined on its output:
+ *   - coefficients stored de-zigzagged, natural order (vp8_tokens.c:337);
+ *   - skipped MBs and Y2-less MBs get explicit zeros (vp8_tokens.c:445-461, :496-502);
+ *   - a block "has coefficients" iff some decoded value is non-zero (vp8_tokens.c:331-339), and
+ *     that flag (not the EOB position) drives the neighbour context (vp8_tokens.c:290, :473-474);
+ *   - has_coeff[mb] = any block of the MB has a non-zero value (vp8_tokens.c:604);
+ *   - non-B_PRED MBs get bmode[] filled with the implied sub-block mode (vp8_tokens.c:913-918);
+ *   - only one token partition is supported; more fail with ENOTSUP (vp8_tokens.c:357-360);
+ *   - the FNV-1a-64 coefficient hash and Vp8CoeffStats counters (vp8_tokens.c:970-998).
+ * All decoder state lives in a per-call context (reentrant, thread-safe).
+ */
+#include <errno.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "vp8_bool.h"
+#include "vp8_front.h"
+
+#include "vp8_tables.inc"
+
+/* ---- RFC 6386 constants --------------------------------------------------------------- */
+
+enum { TOK_ZERO = 0, TOK_ONE, TOK_TWO, TOK_THREE, TOK_FOUR, TOK_CAT1, TOK_CAT2, TOK_CAT3, TOK_CAT4,
+       TOK_CAT5, TOK_CAT6, TOK_EOB };
+
+/* RFC 6386 13.2 token tree */
+static const int8_t k_token_tree[22] = {
+    -TOK_EOB, 2, -TOK_ZERO, 4, -TOK_ONE, 6, 8, 12, -TOK_TWO, 10, -TOK_THREE, -TOK_FOUR,
+    14, 16, -TOK_CAT1, -TOK_CAT2, 18, 20, -TOK_CAT3, -TOK_CAT4, -TOK_CAT5, -TOK_CAT6,
+};
+/* RFC 6386 13.3 band of each scan position, and zigzag scan -> natural index */
+static const uint8_t k_band[17] = {0, 1, 2, 3, 6, 4, 5, 6, 6, 6, 6, 6, 6, 6, 6, 7, 0};
+static const uint8_t k_scan[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
+/* RFC 6386 13.2 extra-bit probabilities of DCT_CAT1..6 (0-terminated) and base values */
+static const uint8_t k_cat_probs[6][12] = {
+    {159, 0}, {165, 145, 0}, {173, 148, 140, 0}, {176, 155, 140, 135, 0}, {180, 157, 141, 134, 130, 0},
+    {254, 254, 243, 230, 196, 177, 153, 140, 133, 130, 129, 0},
+};
+static const int k_cat_base[6] = {5, 7, 11, 19, 35, 67};
+
+/* RFC 6386 11.2 key-frame luma / chroma mode trees (symbols: DC=0 V=1 H=2 TM=3 B=4) */
+static const int8_t k_kf_ymode_tree[8] = {-4, 2, 4, 6, -0, -1, -2, -3};
+static const uint8_t k_kf_ymode_prob[4] = {145, 156, 163, 128};
+static const int8_t k_uv_mode_tree[6] = {-0, 2, -1, 4, -2, -3};
+static const uint8_t k_kf_uv_mode_prob[3] = {142, 114, 183};
+/* RFC 6386 11.2 sub-block mode tree (B_DC=0 TM VE HE LD RD VR VL HD HU=9) */
+static const int8_t k_bmode_tree[18] = {-0, 2, -1, 4, -2, 6, 8, 12, -3, 10, -5, -6, -4, 14, -7, 16, -8, -9};
+/* RFC 6386 9.3 segment id tree */
+static const int8_t k_segment_tree[6] = {2, 4, -0, -1, -2, -3};
+
+enum { PLANE_Y_AFTER_Y2 = 0, PLANE_Y2 = 1, PLANE_UV = 2, PLANE_Y_ALONE = 3 };
+
+/* ---- FNV-1a 64 (same constants as the reference's coefficient hash) ---------------------- */
+
+uint64_t vp8f_fnv1a64(const void* data, size_t n, uint64_t h) {
+	const uint8_t* p = (const uint8_t*)data;
+	for (size_t i = 0; i < n; i++) {
+		h ^= p[i];
+		h *= 1099511628211ull;
+	}
+	return h;
+}
+
+static inline uint64_t hash_block(uint64_t h, const int16_t* blk) {
+	for (int i = 0; i < 16; i++) {
+		uint32_t v = (uint32_t)(int32_t)blk[i];
+		uint8_t le[4] = {(uint8_t)v, (uint8_t)(v >> 8), (uint8_t)(v >> 16), (uint8_t)(v >> 24)};
+		h = vp8f_fnv1a64(le, 4, h);
+	}
+	return h;
+}
+
+/* ---- decoder context -------------------------------------------------------------------- */
+
+typedef struct {
+	uint8_t probs[4][8][3][11]; /* token probabilities after this frame's updates */
+	Vp8Bool tok;                /* token partition */
+	Vp8CoeffStats* st;
+	uint64_t hash;
+} TokenCtx;
+
+static void note_overread(TokenCtx* t, uint32_t mb, uint32_t plane, uint32_t blk, uint32_t pos, uint32_t stage) {
+	Vp8CoeffStats* st = t->st;
+	if (st->token_overread_mb_index != 0xFFFFFFFFu) return;
+	if (vp8b_ref_overread_bytes(&t->tok) == 0) return;
+	st->token_overread_mb_index = mb;
+	st->token_overread_plane = plane;
+	st->token_overread_block_index = blk;
+	st->token_overread_coeff_i = pos;
+	st->token_overread_stage = stage;
+}
+
+/* Decodes one 4x4 block's tokens (RFC 6386 13).  Returns 1 if some value is non-zero.
+ * `plane_tag` is only for the overread diagnostics (0=Y 1=Y2 2=U 3=V). */
+static int read_block(TokenCtx* t, int type, int first, int ctx, int16_t out[16], uint32_t mb, uint32_t plane_tag,
+                      uint32_t blk) {
+	Vp8CoeffStats* st = t->st;
+	memset(out, 0, 16 * sizeof(int16_t));
+	int nonzero = 0;
+	int after_zero = 0;
+	for (int pos = first; pos < 16; pos++) {
+		const uint8_t* p = t->probs[type][k_band[pos]][ctx];
+		int tok = vp8b_tree(&t->tok, k_token_tree, p, after_zero ? 2 : 0);
+		note_overread(t, mb, plane_tag, blk, (uint32_t)pos, 0);
+		if (tok == TOK_EOB) {
+			st->coeff_eob_tokens++;
+			break;
+		}
+		int mag = tok; /* ZERO..FOUR are their own magnitude */
+		if (tok >= TOK_CAT1) {
+			const uint8_t* ep = k_cat_probs[tok - TOK_CAT1];
+			int extra = 0;
+			for (; *ep; ep++) extra = (extra << 1) | vp8b_read(&t->tok, *ep);
+			note_overread(t, mb, plane_tag, blk, (uint32_t)pos, 1);
+			mag = k_cat_base[tok - TOK_CAT1] + extra;
+		}
+		if (mag) {
+			int neg = vp8b_read(&t->tok, 128);
+			note_overread(t, mb, plane_tag, blk, (uint32_t)pos, 2);
+			out[k_scan[pos]] = (int16_t)(neg ? -mag : mag);
+			nonzero = 1;
+			st->coeff_nonzero_total++;
+			if ((uint32_t)mag > st->coeff_abs_max) st->coeff_abs_max = (uint32_t)mag;
+		}
+		ctx = mag == 0 ? 0 : (mag == 1 ? 1 : 2);
+		after_zero = (tok == TOK_ZERO);
+	}
+	return nonzero;
+}
+
+/* Per-MB token decode over the whole frame (RFC 6386 13, reference vp8_tokens.c:354-622). */
+static int read_all_tokens(TokenCtx* t, Vp8DecodedFrame* f, const uint8_t* has_y2) {
+	const uint32_t cols = f->mb_cols;
+	uint8_t* above = (uint8_t*)calloc((size_t)cols, 9); /* per MB column: Y[4] U[2] V[2] Y2 */
+	if (!above) {
+		errno = ENOMEM;
+		return -1;
+	}
+	Vp8CoeffStats* st = t->st;
+	for (uint32_t r = 0; r < f->mb_rows; r++) {
+		uint8_t left[9] = {0};
+		for (uint32_t c = 0; c < cols; c++) {
+			const uint32_t mb = r * cols + c;
+			uint8_t* ab = above + (size_t)c * 9;
+			const int skip = f->skip_coeff[mb];
+			int any = 0;
+			int16_t* y2 = f->coeff_y2 + (size_t)mb * 16;
+			if (has_y2[mb]) {
+				st->blocks_total_y2++;
+				int nz = 0;
+				if (!skip) nz = read_block(t, PLANE_Y2, 0, left[8] + ab[8], y2, mb, 1, 0);
+				else memset(y2, 0, 32);
+				t->hash = hash_block(t->hash, y2);
+				st->blocks_nonzero_y2 += (uint32_t)nz;
+				any |= nz;
+				left[8] = ab[8] = (uint8_t)nz;
+			} else {
+				memset(y2, 0, 32);
+			}
+			const int ytype = has_y2[mb] ? PLANE_Y_AFTER_Y2 : PLANE_Y_ALONE;
+			const int yfirst = has_y2[mb] ? 1 : 0;
+			for (int by = 0; by < 4; by++) {
+				for (int bx = 0; bx < 4; bx++) {
+					int16_t* blk = f->coeff_y + ((size_t)mb * 16 + (size_t)(by * 4 + bx)) * 16;
+					st->blocks_total_y++;
+					int nz = 0;
+					if (!skip) nz = read_block(t, ytype, yfirst, left[by] + ab[bx], blk, mb, 0, (uint32_t)(by * 4 + bx));
+					else memset(blk, 0, 32);
+					t->hash = hash_block(t->hash, blk);
+					st->blocks_nonzero_y += (uint32_t)nz;
+					any |= nz;
+					left[by] = ab[bx] = (uint8_t)nz;
+				}
+			}
+			for (int pl = 0; pl < 2; pl++) { /* U then V */
+				int16_t* base = (pl == 0 ? f->coeff_u : f->coeff_v) + (size_t)mb * 64;
+				uint8_t* lc = left + 4 + 2 * pl;
+				uint8_t* ac = ab + 4 + 2 * pl;
+				for (int by = 0; by < 2; by++) {
+					for (int bx = 0; bx < 2; bx++) {
+						int16_t* blk = base + (by * 2 + bx) * 16;
+						int nz = 0;
+						if (!skip)
+							nz = read_block(t, PLANE_UV, 0, lc[by] + ac[bx], blk, mb, (uint32_t)(2 + pl),
+							                (uint32_t)(by * 2 + bx));
+						else memset(blk, 0, 32);
+						t->hash = hash_block(t->hash, blk);
+						if (pl == 0) {
+							st->blocks_total_u++;
+							st->blocks_nonzero_u += (uint32_t)nz;
+						} else {
+							st->blocks_total_v++;
+							st->blocks_nonzero_v += (uint32_t)nz;
+						}
+						any |= nz;
+						lc[by] = ac[bx] = (uint8_t)nz;
+					}
+				}
+			}
+			f->has_coeff[mb] = (uint8_t)(any != 0);
+		}
+	}
+	free(above);
+	st->token_part_bytes_used = (uint32_t)vp8b_ref_bytes_used(&t->tok);
+	st->token_overread_bytes = vp8b_ref_overread_bytes(&t->tok);
+	st->token_overread = (uint8_t)(st->token_overread_bytes != 0);
+	return 0;
+}
+
+void vp8_decoded_frame_free(Vp8DecodedFrame* f) {
+	if (!f) return;
+	free(f->segment_id);
+	free(f->skip_coeff);
+	free(f->has_coeff);
+	free(f->ymode);
+	free(f->uv_mode);
+	free(f->bmode);
+	free(f->coeff_y2);
+	free(f->coeff_y);
+	free(f->coeff_u);
+	free(f->coeff_v);
+	memset(f, 0, sizeof(*f));
+}
+
+static int8_t clamp_s8(int32_t v) { return (int8_t)(v < -128 ? -128 : (v > 127 ? 127 : v)); }
+
+/* optional signed field: flag, then magnitude + sign (RFC 6386 9.3, 9.6) */
+static int8_t read_opt_signed(Vp8Bool* b, int nbits) {
+	if (!vp8b_read(b, 128)) return 0;
+	return clamp_s8(vp8b_signed(b, nbits));
+}
+
+int vp8_decode_decoded_frame(ByteSpan payload, Vp8DecodedFrame* out) {
+	if (!out) return -1;
+	memset(out, 0, sizeof(*out));
+	Vp8KeyFrameHeader kf;
+	if (vp8_parse_keyframe_header(payload, &kf) != 0) {
+		errno = EINVAL;
+		return -1;
+	}
+	if (!kf.is_key_frame) {
+		errno = ENOTSUP;
+		return -1;
+	}
+	const uint32_t cols = (kf.width + 15u) >> 4, rows = (kf.height + 15u) >> 4;
+	const uint32_t total = cols * rows;
+	Vp8CoeffStats* st = &out->stats;
+	out->mb_cols = st->mb_cols = cols;
+	out->mb_rows = st->mb_rows = rows;
+	out->mb_total = st->mb_total = total;
+	st->token_overread_mb_index = st->token_overread_plane = st->token_overread_block_index = 0xFFFFFFFFu;
+	st->token_overread_coeff_i = st->token_overread_stage = 0xFFFFFFFFu;
+	if (cols == 0 || rows == 0 || total > (1u << 20)) {
+		errno = EINVAL;
+		return -1;
+	}
+
+	out->segment_id = (uint8_t*)calloc(total, 1);
+	out->skip_coeff = (uint8_t*)calloc(total, 1);
+	out->has_coeff = (uint8_t*)calloc(total, 1);
+	out->ymode = (uint8_t*)calloc(total, 1);
+	out->uv_mode = (uint8_t*)calloc(total, 1);
+	out->bmode = (uint8_t*)calloc((size_t)total * 16, 1);
+	out->coeff_y2 = (int16_t*)calloc((size_t)total * 16, sizeof(int16_t));
+	out->coeff_y = (int16_t*)calloc((size_t)total * 256, sizeof(int16_t));
+	out->coeff_u = (int16_t*)calloc((size_t)total * 64, sizeof(int16_t));
+	out->coeff_v = (int16_t*)calloc((size_t)total * 64, sizeof(int16_t));
+	uint8_t* has_y2 = (uint8_t*)calloc(total, 1);
+	uint8_t* above_b = (uint8_t*)calloc((size_t)cols * 4, 1); /* above sub-block modes, B_DC = 0 */
+	TokenCtx* t = (TokenCtx*)calloc(1, sizeof(TokenCtx));
+	int rc = -1;
+	if (!out->segment_id || !out->skip_coeff || !out->has_coeff || !out->ymode || !out->uv_mode || !out->bmode ||
+	    !out->coeff_y2 || !out->coeff_y || !out->coeff_u || !out->coeff_v || !has_y2 || !above_b || !t) {
+		errno = ENOMEM;
+		goto done;
+	}
+	if (payload.size < 10u + kf.first_partition_len) {
+		errno = EINVAL;
+		goto done;
+	}
+
+	Vp8Bool hb;
+	vp8b_init(&hb, payload.data + 10, kf.first_partition_len);
+	st->part0_size_bytes = kf.first_partition_len;
+	(void)vp8b_read(&hb, 128); /* color space */
+	(void)vp8b_read(&hb, 128); /* clamping type */
+
+	/* RFC 6386 9.3 segmentation */
+	int seg_map_update = 0;
+	uint8_t seg_probs[3] = {255, 255, 255};
+	out->segmentation_enabled = (uint8_t)vp8b_read(&hb, 128);
+	if (out->segmentation_enabled) {
+		seg_map_update = vp8b_read(&hb, 128);
+		if (vp8b_read(&hb, 128)) { /* update_segment_feature_data */
+			out->segmentation_abs = (uint8_t)vp8b_read(&hb, 128);
+			for (int i = 0; i < 4; i++) out->seg_quant_idx[i] = read_opt_signed(&hb, 7);
+			for (int i = 0; i < 4; i++) out->seg_lf_level[i] = read_opt_signed(&hb, 6);
+		}
+		if (seg_map_update)
+			for (int i = 0; i < 3; i++)
+				if (vp8b_read(&hb, 128)) seg_probs[i] = (uint8_t)vp8b_literal(&hb, 8);
+	}
+
+	/* RFC 6386 9.6 loop filter */
+	out->lf_use_simple = (uint8_t)vp8b_read(&hb, 128);
+	out->lf_level = (uint8_t)vp8b_literal(&hb, 6);
+	out->lf_sharpness = (uint8_t)vp8b_literal(&hb, 3);
+	out->lf_delta_enabled = (uint8_t)vp8b_read(&hb, 128);
+	if (out->lf_delta_enabled && vp8b_read(&hb, 128)) {
+		for (int i = 0; i < 4; i++) out->lf_ref_delta[i] = read_opt_signed(&hb, 6);
+		for (int i = 0; i < 4; i++) out->lf_mode_delta[i] = read_opt_signed(&hb, 6);
+	}
+
+	/* RFC 6386 9.5 token partitions */
+	const unsigned nparts = 1u << vp8b_literal(&hb, 2);
+
+	/* RFC 6386 9.6 quantisation */
+	out->q_index = (uint8_t)vp8b_literal(&hb, 7);
+	out->y1_dc_delta_q = read_opt_signed(&hb, 4);
+	out->y2_dc_delta_q = read_opt_signed(&hb, 4);
+	out->y2_ac_delta_q = read_opt_signed(&hb, 4);
+	out->uv_dc_delta_q = read_opt_signed(&hb, 4);
+	out->uv_ac_delta_q = read_opt_signed(&hb, 4);
+	(void)vp8b_read(&hb, 128); /* refresh_entropy_probs */
+
+	/* RFC 6386 13.4 token probability updates */
+	memcpy(t->probs, vp8_default_coeff_probs, sizeof(t->probs));
+	for (int i = 0; i < 4; i++)
+		for (int j = 0; j < 8; j++)
+			for (int k = 0; k < 3; k++)
+				for (int l = 0; l < 11; l++)
+					if (vp8b_read(&hb, vp8_coeff_update_probs[i][j][k][l])) t->probs[i][j][k][l] = (uint8_t)vp8b_literal(&hb, 8);
+
+	const int use_skip = vp8b_read(&hb, 128);
+	const uint8_t skip_prob = use_skip ? (uint8_t)vp8b_literal(&hb, 8) : 0;
+
+	/* RFC 6386 11 / 19.3 per-macroblock header */
+	for (uint32_t r = 0; r < rows; r++) {
+		uint8_t left_b[4] = {0, 0, 0, 0};
+		for (uint32_t c = 0; c < cols; c++) {
+			const uint32_t mb = r * cols + c;
+			if (out->segmentation_enabled && seg_map_update)
+				out->segment_id[mb] = (uint8_t)vp8b_tree(&hb, k_segment_tree, seg_probs, 0);
+			if (use_skip) out->skip_coeff[mb] = (uint8_t)vp8b_read(&hb, skip_prob);
+			st->mb_skip_coeff += out->skip_coeff[mb];
+			const int ym = vp8b_tree(&hb, k_kf_ymode_tree, k_kf_ymode_prob, 0);
+			out->ymode[mb] = (uint8_t)ym;
+			st->ymode_counts[ym]++;
+			uint8_t* bm = out->bmode + (size_t)mb * 16;
+			uint8_t* ab = above_b + (size_t)c * 4;
+			if (ym == 4) {
+				st->mb_b_pred++;
+				for (int i = 0; i < 16; i++) {
+					const int y = i >> 2, x = i & 3;
+					const uint8_t a = y ? bm[i - 4] : ab[x];
+					const uint8_t l = x ? bm[i - 1] : left_b[y];
+					bm[i] = (uint8_t)vp8b_tree(&hb, k_bmode_tree, vp8_kf_bmode_prob[a][l], 0);
+					st->bmode_counts[bm[i]]++;
+				}
+				for (int i = 0; i < 4; i++) {
+					ab[i] = bm[12 + i];
+					left_b[i] = bm[4 * i + 3];
+				}
+			} else {
+				/* implied sub-block context: DC->B_DC, V->B_VE, H->B_HE, TM->B_TM */
+				static const uint8_t implied[4] = {0, 2, 3, 1};
+				memset(bm, implied[ym], 16);
+				memset(ab, implied[ym], 4);
+				memset(left_b, implied[ym], 4);
+				has_y2[mb] = 1;
+			}
+			const int uvm = vp8b_tree(&hb, k_uv_mode_tree, k_kf_uv_mode_prob, 0);
+			out->uv_mode[mb] = (uint8_t)uvm;
+			st->uv_mode_counts[uvm]++;
+		}
+	}
+	st->part0_bytes_used = (uint32_t)vp8b_ref_bytes_used(&hb);
+	st->part0_overread_bytes = vp8b_ref_overread_bytes(&hb);
+	st->part0_overread = (uint8_t)(st->part0_overread_bytes != 0);
+
+	if (nparts != 1) {
+		errno = ENOTSUP;
+		goto done;
+	}
+	const size_t tok_off = 10u + kf.first_partition_len;
+	vp8b_init(&t->tok, payload.data + tok_off, payload.size - tok_off);
+	st->token_part_size_bytes = (uint32_t)(payload.size - tok_off);
+	t->st = st;
+	t->hash = 1469598103934665603ull;
+	if (read_all_tokens(t, out, has_y2) != 0) goto done;
+	st->coeff_hash_fnv1a64 = t->hash;
+	rc = 0;
+
+done:
+	free(has_y2);
+	free(above_b);
+	free(t);
+	if (rc != 0) {
+		int e = errno;
+		vp8_decoded_frame_free(out);
+		errno = e;
+	}
+	return rc;
+}

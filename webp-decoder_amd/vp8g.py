@@ -1,0 +1,347 @@
+"""vp8g -- Python mirror of the C ABI in include/vp8g.h (ctypes; no torch types cross it).
+
+Loads the in-tree libraries built by the top-level Makefile:
+  lib/libvp8host.so  C11 front end (reference m01-m05 equivalents) + synthetic frame generator
+  lib/libvp8g.so     HIP gfx950 kernels behind the reference's m06/m07 entry points + batch API
+
+The structures below are layout-identical to the reference's (reference src/m02_vp8_header/
+vp8_header.h:7-18, src/m05_tokens/vp8_tokens.h:7-99, src/m06_recon/vp8_recon.h:10-18), so a
+Vp8DecodedFrame produced by either front end can be handed to either reconstruction library.
+
+Nothing here falls back to the CPU: if libvp8g.so (or a GPU) is missing, the GPU entry points
+raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import pathlib
+
+import numpy as np
+
+PKG_DIR = pathlib.Path(__file__).resolve().parent
+REPO_DIR = PKG_DIR.parent
+LIB_DIR = PKG_DIR / "lib"
+
+
+class ByteSpan(C.Structure):
+    _fields_ = [("data", C.POINTER(C.c_uint8)), ("size", C.c_size_t)]
+
+
+class Vp8KeyFrameHeader(C.Structure):
+    _fields_ = [
+        ("is_key_frame", C.c_int),
+        ("profile", C.c_uint8),
+        ("show_frame", C.c_int),
+        ("first_partition_len", C.c_uint32),
+        ("start_code_ok", C.c_int),
+        ("width", C.c_uint16),
+        ("height", C.c_uint16),
+        ("x_scale", C.c_uint8),
+        ("y_scale", C.c_uint8),
+    ]
+
+
+class Vp8CoeffStats(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in (
+        "mb_cols", "mb_rows", "mb_total", "part0_size_bytes", "part0_bytes_used")] + [
+        ("part0_overread", C.c_uint8), ("part0_overread_bytes", C.c_uint32),
+        ("token_part_size_bytes", C.c_uint32), ("token_part_bytes_used", C.c_uint32),
+        ("token_overread", C.c_uint8)] + [(n, C.c_uint32) for n in (
+            "token_overread_bytes", "token_overread_mb_index", "token_overread_plane",
+            "token_overread_block_index", "token_overread_coeff_i", "token_overread_stage",
+            "mb_skip_coeff", "mb_b_pred")] + [
+        ("ymode_counts", C.c_uint32 * 5), ("uv_mode_counts", C.c_uint32 * 4),
+        ("bmode_counts", C.c_uint32 * 10)] + [(n, C.c_uint32) for n in (
+            "blocks_total_y2", "blocks_total_y", "blocks_total_u", "blocks_total_v",
+            "blocks_nonzero_y2", "blocks_nonzero_y", "blocks_nonzero_u", "blocks_nonzero_v",
+            "coeff_nonzero_total", "coeff_eob_tokens", "coeff_abs_max")] + [
+        ("coeff_hash_fnv1a64", C.c_uint64)]
+
+
+class Vp8DecodedFrame(C.Structure):
+    _fields_ = [
+        ("mb_cols", C.c_uint32), ("mb_rows", C.c_uint32), ("mb_total", C.c_uint32),
+        ("q_index", C.c_uint8), ("y1_dc_delta_q", C.c_int8), ("y2_dc_delta_q", C.c_int8),
+        ("y2_ac_delta_q", C.c_int8), ("uv_dc_delta_q", C.c_int8), ("uv_ac_delta_q", C.c_int8),
+        ("segmentation_enabled", C.c_uint8), ("segmentation_abs", C.c_uint8),
+        ("seg_quant_idx", C.c_int8 * 4), ("seg_lf_level", C.c_int8 * 4),
+        ("lf_use_simple", C.c_uint8), ("lf_level", C.c_uint8), ("lf_sharpness", C.c_uint8),
+        ("lf_delta_enabled", C.c_uint8), ("lf_ref_delta", C.c_int8 * 4), ("lf_mode_delta", C.c_int8 * 4),
+        ("segment_id", C.POINTER(C.c_uint8)), ("skip_coeff", C.POINTER(C.c_uint8)),
+        ("has_coeff", C.POINTER(C.c_uint8)), ("ymode", C.POINTER(C.c_uint8)),
+        ("uv_mode", C.POINTER(C.c_uint8)), ("bmode", C.POINTER(C.c_uint8)),
+        ("coeff_y2", C.POINTER(C.c_int16)), ("coeff_y", C.POINTER(C.c_int16)),
+        ("coeff_u", C.POINTER(C.c_int16)), ("coeff_v", C.POINTER(C.c_int16)),
+        ("stats", Vp8CoeffStats),
+    ]
+
+
+class Yuv420Image(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("stride_y", C.c_uint32),
+                ("stride_uv", C.c_uint32), ("y", C.POINTER(C.c_uint8)), ("u", C.POINTER(C.c_uint8)),
+                ("v", C.POINTER(C.c_uint8))]
+
+
+class Vp8gFrameDesc(C.Structure):
+    _fields_ = [
+        ("mb_cols", C.c_uint32), ("mb_rows", C.c_uint32), ("width", C.c_uint32), ("height", C.c_uint32),
+        ("stride_y", C.c_uint32), ("stride_uv", C.c_uint32), ("mb_offset", C.c_uint64),
+        ("out_y", C.c_uint64), ("out_u", C.c_uint64), ("out_v", C.c_uint64),
+        ("src_y", C.c_uint64), ("src_u", C.c_uint64), ("src_v", C.c_uint64),
+        ("flags", C.c_uint32), ("src_stride_y", C.c_uint32), ("src_stride_uv", C.c_uint32),
+        ("reserved", C.c_uint32), ("dq", (C.c_int16 * 6) * 4), ("lf", ((C.c_uint8 * 4) * 2) * 4),
+    ]
+
+
+class Vp8gBatchArrays(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in (
+        "coeff_y", "coeff_u", "coeff_v", "coeff_y2", "ymode", "uv_mode", "segment_id", "has_coeff",
+        "bmode", "src", "status")]
+
+
+assert C.sizeof(Vp8KeyFrameHeader) == 28
+assert C.sizeof(Vp8CoeffStats) == 200
+assert C.sizeof(Vp8DecodedFrame) == 320
+assert C.sizeof(Yuv420Image) == 40
+assert C.sizeof(Vp8gFrameDesc) == 176
+
+VP8G_F_LOOPFILTER = 1
+VP8G_F_SIMPLE = 2
+VP8G_F_LF_ONLY = 4
+
+# Arrays of a decoded frame: (field, dtype, elements per MB)
+FRAME_ARRAYS = [
+    ("coeff_y", np.int16, 256), ("coeff_u", np.int16, 64), ("coeff_v", np.int16, 64),
+    ("coeff_y2", np.int16, 16), ("ymode", np.uint8, 1), ("uv_mode", np.uint8, 1),
+    ("segment_id", np.uint8, 1), ("has_coeff", np.uint8, 1), ("bmode", np.uint8, 16),
+    ("skip_coeff", np.uint8, 1),
+]
+# Algorithmic bytes the hot path reads per macroblock: 800 B of dense int16
+# coefficients + 20 B side info (ymode, uv_mode, segment_id, has_coeff, 16 x bmode).
+BYTES_READ_PER_MB = 820
+
+
+def i420_size(w: int, h: int) -> int:
+    return w * h + 2 * ((w + 1) // 2) * ((h + 1) // 2)
+
+
+_libs: dict = {}
+
+
+def _load(name: str, path: pathlib.Path):
+    if name not in _libs:
+        if not path.exists():
+            raise OSError(f"{path} not built (run `make` at the repo root)")
+        _libs[name] = C.CDLL(str(path))
+    return _libs[name]
+
+
+def host_lib():
+    lib = _load("host", LIB_DIR / "libvp8host.so")
+    if not getattr(lib, "_typed", False):
+        lib.vp8f_decode_file.argtypes = [C.c_char_p, C.POINTER(Vp8KeyFrameHeader), C.POINTER(Vp8DecodedFrame),
+                                         C.POINTER(C.c_int)]
+        lib.vp8f_decode_memory.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(Vp8KeyFrameHeader),
+                                           C.POINTER(Vp8DecodedFrame), C.POINTER(C.c_int)]
+        lib.vp8f_synth_frame.argtypes = [C.c_uint32, C.c_uint32, C.c_uint64, C.c_int, C.POINTER(Vp8KeyFrameHeader),
+                                         C.POINTER(Vp8DecodedFrame)]
+        lib.vp8_decoded_frame_free.argtypes = [C.POINTER(Vp8DecodedFrame)]
+        lib.vp8_decoded_frame_free.restype = None
+        lib.vp8f_fnv1a64.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64]
+        lib.vp8f_fnv1a64.restype = C.c_uint64
+        lib._typed = True
+    return lib
+
+
+def gpu_lib():
+    """libvp8g.so: the product path.  Raises if it is not built."""
+    lib = _load("gpu", LIB_DIR / "libvp8g.so")
+    if not getattr(lib, "_typed", False):
+        P = C.POINTER
+        lib.vp8_reconstruct_keyframe_yuv.argtypes = [P(Vp8KeyFrameHeader), P(Vp8DecodedFrame), P(Yuv420Image)]
+        lib.vp8_reconstruct_keyframe_yuv_filtered.argtypes = [P(Vp8KeyFrameHeader), P(Vp8DecodedFrame),
+                                                              P(Yuv420Image)]
+        lib.vp8_loopfilter_apply_keyframe.argtypes = [P(Yuv420Image), P(Vp8DecodedFrame)]
+        lib.yuv420_alloc.argtypes = [P(Yuv420Image), C.c_uint32, C.c_uint32]
+        lib.yuv420_free.argtypes = [P(Yuv420Image)]
+        lib.yuv420_free.restype = None
+        lib.vp8g_make_frame_desc.argtypes = [P(Vp8KeyFrameHeader), P(Vp8DecodedFrame), C.c_int, C.c_uint64,
+                                             C.c_uint64, P(Vp8gFrameDesc)]
+        lib.vp8g_i420_size.argtypes = [C.c_uint32, C.c_uint32]
+        lib.vp8g_i420_size.restype = C.c_uint64
+        lib.vp8g_decode_batch_device.argtypes = [P(Vp8gFrameDesc), C.c_void_p, C.c_uint32, P(Vp8gBatchArrays),
+                                                 C.c_void_p, C.c_void_p, C.c_uint32]
+        lib.vp8g_reconstruct_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int, P(Yuv420Image)]
+        lib.vp8g_last_error.restype = C.c_char_p
+        lib.vp8g_abi_version.restype = C.c_uint32
+        lib._typed = True
+    return lib
+
+
+class Frame:
+    """Owns one Vp8DecodedFrame (+ its key-frame header) allocated by libvp8host."""
+
+    def __init__(self, kf: Vp8KeyFrameHeader, frame: Vp8DecodedFrame):
+        self.kf = kf
+        self.frame = frame
+        self._alive = True
+
+    @property
+    def width(self) -> int:
+        return int(self.kf.width)
+
+    @property
+    def height(self) -> int:
+        return int(self.kf.height)
+
+    @property
+    def mb_total(self) -> int:
+        return int(self.frame.mb_total)
+
+    def array(self, name: str) -> np.ndarray:
+        for n, dt, per in FRAME_ARRAYS:
+            if n == name:
+                ptr = getattr(self.frame, name)
+                if not ptr:
+                    return np.zeros(self.mb_total * per, dtype=dt)
+                return np.ctypeslib.as_array(ptr, shape=(self.mb_total * per,)).view(dt)
+        raise KeyError(name)
+
+    def free(self):
+        if self._alive:
+            host_lib().vp8_decoded_frame_free(C.byref(self.frame))
+            self._alive = False
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def decode_file(path) -> Frame:
+    lib = host_lib()
+    kf, fr, st = Vp8KeyFrameHeader(), Vp8DecodedFrame(), C.c_int(0)
+    if lib.vp8f_decode_file(str(path).encode(), C.byref(kf), C.byref(fr), C.byref(st)) != 0:
+        raise ValueError(f"decode failed at stage {st.value}: {path}")
+    return Frame(kf, fr)
+
+
+def synth_frame(width: int, height: int, seed: int, profile: int = 0) -> Frame:
+    lib = host_lib()
+    kf, fr = Vp8KeyFrameHeader(), Vp8DecodedFrame()
+    if lib.vp8f_synth_frame(width, height, seed & 0xFFFFFFFFFFFFFFFF, profile, C.byref(kf), C.byref(fr)) != 0:
+        raise ValueError("synth failed")
+    return Frame(kf, fr)
+
+
+def fnv1a64(buf: bytes | np.ndarray, h: int = 1469598103934665603) -> int:
+    b = np.ascontiguousarray(np.frombuffer(buf, dtype=np.uint8) if isinstance(buf, (bytes, bytearray)) else buf)
+    return int(host_lib().vp8f_fnv1a64(b.ctypes.data, b.nbytes, h))
+
+
+def _image_bytes(img: Yuv420Image) -> bytes:
+    ysz = img.stride_y * img.height
+    uvsz = img.stride_uv * ((img.height + 1) // 2)
+    return C.string_at(img.y, ysz) + C.string_at(img.u, uvsz) + C.string_at(img.v, uvsz)
+
+
+def gpu_reconstruct(f: Frame, filtered: bool) -> bytes:
+    """Reference entry point vp8_reconstruct_keyframe_yuv[_filtered] through libvp8g.so."""
+    lib = gpu_lib()
+    img = Yuv420Image()
+    fn = lib.vp8_reconstruct_keyframe_yuv_filtered if filtered else lib.vp8_reconstruct_keyframe_yuv
+    if fn(C.byref(f.kf), C.byref(f.frame), C.byref(img)) != 0:
+        raise RuntimeError(f"vp8g reconstruction failed: errno={C.get_errno()} {lib.vp8g_last_error()!r}")
+    try:
+        return _image_bytes(img)
+    finally:
+        lib.yuv420_free(C.byref(img))
+
+
+def gpu_reconstruct_batch(frames: list[Frame], filtered: bool) -> list[bytes]:
+    lib = gpu_lib()
+    n = len(frames)
+    kfs = (C.POINTER(Vp8KeyFrameHeader) * n)(*[C.pointer(f.kf) for f in frames])
+    frs = (C.POINTER(Vp8DecodedFrame) * n)(*[C.pointer(f.frame) for f in frames])
+    imgs = (Yuv420Image * n)()
+    if lib.vp8g_reconstruct_batch(C.cast(kfs, C.c_void_p), C.cast(frs, C.c_void_p), n, int(filtered), imgs) != 0:
+        raise RuntimeError(f"vp8g batch failed: {lib.vp8g_last_error()!r}")
+    out = []
+    for i in range(n):
+        out.append(_image_bytes(imgs[i]))
+        lib.yuv420_free(C.byref(imgs[i]))
+    return out
+
+
+def make_desc(f: Frame, filtered: bool, mb_offset: int, out_offset: int) -> Vp8gFrameDesc:
+    d = Vp8gFrameDesc()
+    if gpu_lib().vp8g_make_frame_desc(C.byref(f.kf), C.byref(f.frame), int(filtered), mb_offset, out_offset,
+                                      C.byref(d)) != 0:
+        raise ValueError("vp8g_make_frame_desc failed")
+    return d
+
+
+# ---- test/bench-only loaders (oracle/ is test infrastructure) ------------------------------
+
+def oracle_lib():
+    lib = _load("oracle", REPO_DIR / "oracle" / "liboracle.so")
+    if not getattr(lib, "_typed", False):
+        P = C.POINTER
+        lib.oracle_reconstruct_i420.argtypes = [P(Vp8KeyFrameHeader), P(Vp8DecodedFrame), C.c_void_p, C.c_int]
+        lib.oracle_recon_padded.argtypes = [P(Vp8DecodedFrame), C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        lib.oracle_loopfilter.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, P(Vp8DecodedFrame)]
+        lib.oracle_time_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int]
+        lib.oracle_time_batch.restype = C.c_double
+        lib._typed = True
+    return lib
+
+
+def oracle_reconstruct(f: Frame, filtered: bool) -> bytes:
+    buf = np.empty(i420_size(f.width, f.height), dtype=np.uint8)
+    if oracle_lib().oracle_reconstruct_i420(C.byref(f.kf), C.byref(f.frame), buf.ctypes.data, int(filtered)) != 0:
+        raise RuntimeError("oracle failed")
+    return buf.tobytes()
+
+
+def ref_lib():
+    """oracle/_ref/libref.so: the reference's own m01-m07 compiled here (may be absent)."""
+    lib = _load("ref", REPO_DIR / "oracle" / "_ref" / "libref.so")
+    if not getattr(lib, "_typed", False):
+        P = C.POINTER
+        lib.ref_decode_i420.argtypes = [C.c_char_p, C.c_void_p, C.c_size_t, C.c_int]
+        lib.ref_decode_i420.restype = C.c_long
+        lib.ref_recon_i420.argtypes = [P(Vp8KeyFrameHeader), P(Vp8DecodedFrame), C.c_void_p, C.c_int]
+        lib.ref_decode_frame.argtypes = [C.c_char_p, P(Vp8KeyFrameHeader), P(Vp8DecodedFrame)]
+        lib.ref_free_frame.argtypes = [P(Vp8DecodedFrame)]
+        lib.ref_free_frame.restype = None
+        lib.ref_coeff_hash.argtypes = [C.c_char_p]
+        lib.ref_coeff_hash.restype = C.c_uint64
+        lib.ref_loopfilter_padded.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
+                                              P(Vp8DecodedFrame)]
+        lib.ref_time_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int]
+        lib.ref_time_batch.restype = C.c_double
+        lib._typed = True
+    return lib
+
+
+def ref_available() -> bool:
+    return (REPO_DIR / "oracle" / "_ref" / "libref.so").exists()
+
+
+def ref_reconstruct(f: Frame, filtered: bool) -> bytes:
+    buf = np.empty(i420_size(f.width, f.height), dtype=np.uint8)
+    if ref_lib().ref_recon_i420(C.byref(f.kf), C.byref(f.frame), buf.ctypes.data, int(filtered)) != 0:
+        raise RuntimeError("reference recon failed")
+    return buf.tobytes()
+
+
+def cpu_time_batch(frames: list[Frame], n: int, threads: int, filtered: bool, kind: str = "port") -> float:
+    """Seconds for `n` frame reconstructions on `threads` host threads (oracle port or reference)."""
+    lib = oracle_lib() if kind == "port" else ref_lib()
+    fn = lib.oracle_time_batch if kind == "port" else lib.ref_time_batch
+    k = len(frames)
+    kfs = (C.POINTER(Vp8KeyFrameHeader) * k)(*[C.pointer(f.kf) for f in frames])
+    frs = (C.POINTER(Vp8DecodedFrame) * k)(*[C.pointer(f.frame) for f in frames])
+    return float(fn(C.cast(kfs, C.c_void_p), C.cast(frs, C.c_void_p), k, n, threads, int(filtered)))
