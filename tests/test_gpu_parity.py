@@ -1,0 +1,131 @@
+"""GPU parity tests (MI355X): libvp8g.so's HIP path vs the golden manifests and the oracle.
+
+Bar: bit-exact (integer/byte work).  Every call goes through the C ABI (include/vp8g.h): the
+reference entry points for single frames, vp8g_reconstruct_batch for batches, and the device
+batch API in test_gpu_batch.py.
+"""
+import ctypes as C
+import hashlib
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import FIXTURES, ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+def _chunks(seq, n):
+    for i in range(0, len(seq), n):
+        yield seq[i:i + n]
+
+
+@pytest.mark.parametrize("filtered", [False, True], ids=["yuv", "yuvf"])
+def test_corpus_batches_vs_manifest(vp8g, manifest, filtered):
+    """All 441 fixtures (the reference m6/m7 gate corpus + penguins + large frames), batched."""
+    key = "yuvf_sha256" if filtered else "yuv_sha256"
+    rels = sorted(manifest["files"])
+    bad = []
+    for chunk in _chunks(rels, 48):
+        frames = [vp8g.decode_file(FIXTURES / r) for r in chunk]
+        outs = vp8g.gpu_reconstruct_batch(frames, filtered)
+        for r, o in zip(chunk, outs):
+            if sha(o) != manifest["files"][r][key]:
+                bad.append(r)
+        for f in frames:
+            f.free()
+    assert not bad, f"{len(bad)} mismatches, e.g. {bad[:8]}"
+
+
+@pytest.mark.parametrize("rel", ["big/k128_normal.webp", "big/fhd_normal_sharp5.webp", "big/fhd_simple_sharp3.webp",
+                                 "big/uhd_a_normal_seg4.webp", "big/odd_1917x1083_normal.webp",
+                                 "commons/penguin-q80.webp"])
+@pytest.mark.parametrize("filtered", [False, True], ids=["yuv", "yuvf"])
+def test_single_frame_entry_points(vp8g, manifest, rel, filtered):
+    """BASELINE configs 1-3: the reference's own entry points, one frame per call."""
+    f = vp8g.decode_file(FIXTURES / rel)
+    out = vp8g.gpu_reconstruct(f, filtered)
+    assert sha(out) == manifest["files"][rel]["yuvf_sha256" if filtered else "yuv_sha256"]
+
+
+def test_synth_kat(vp8g, synth_kat):
+    """Seeded synthetic frames (stress: full-range coefficients, every mode, random LF params,
+    ignored fields set to garbage) vs the reference m06/m07 hashes."""
+    frames = [vp8g.synth_frame(c["width"], c["height"], c["seed"], c["profile"]) for c in synth_kat["cases"]]
+    for filtered, key in ((False, "yuv_sha256"), (True, "yuvf_sha256")):
+        outs = vp8g.gpu_reconstruct_batch(frames, filtered)
+        for c, o in zip(synth_kat["cases"], outs):
+            assert sha(o) == c[key], (c, key)
+
+
+@pytest.mark.parametrize("profile", [0, 1, 2])
+def test_random_mixed_batch_vs_oracle(vp8g, profile):
+    rng = np.random.default_rng(profile + 7)
+    frames = []
+    for i in range(24):
+        w, h = int(rng.integers(1, 700)), int(rng.integers(1, 500))
+        frames.append(vp8g.synth_frame(w, h, 1000 + 31 * i + profile, profile))
+    for filtered in (False, True):
+        outs = vp8g.gpu_reconstruct_batch(frames, filtered)
+        for f, o in zip(frames, outs):
+            assert o == vp8g.oracle_reconstruct(f, filtered), (f.width, f.height, filtered)
+
+
+@pytest.mark.parametrize("w,h", [(16383, 16), (16, 2000), (8200, 40), (4097, 33)])
+def test_extreme_dimensions(vp8g, w, h):
+    """Maximum VP8 width (14-bit) takes the device-memory context path; tall/narrow frames use
+    one MB column."""
+    f = vp8g.synth_frame(w, h, w * 7 + h, 1)
+    for filtered in (False, True):
+        assert vp8g.gpu_reconstruct(f, filtered) == vp8g.oracle_reconstruct(f, filtered)
+
+
+def test_frames_are_independent_in_a_batch(vp8g, manifest):
+    """Same 4K frame 6x in one batch + a different one between: every copy identical."""
+    a = vp8g.decode_file(FIXTURES / "big/uhd_a_normal_seg4.webp")
+    b = vp8g.decode_file(FIXTURES / "big/uhd_b_simple_sharp3.webp")
+    outs = vp8g.gpu_reconstruct_batch([a, a, b, a, a, b, a, a], True)
+    ha, hb = manifest["files"]["big/uhd_a_normal_seg4.webp"]["yuvf_sha256"], manifest["files"]["big/uhd_b_simple_sharp3.webp"]["yuvf_sha256"]
+    assert [sha(o) for o in outs] == [ha, ha, hb, ha, ha, hb, ha, ha]
+
+
+@pytest.mark.parametrize("seed,profile", [(1, 0), (2, 1), (3, 2)])
+def test_loopfilter_entry_point_vs_oracle(vp8g, seed, profile):
+    """vp8_loopfilter_apply_keyframe (m07 alone, in place on a padded image)."""
+    lib = C.CDLL(str(vp8g.LIB_DIR / "libvp8g.so"), use_errno=True)
+    lib.yuv420_alloc.argtypes = [C.POINTER(vp8g.Yuv420Image), C.c_uint32, C.c_uint32]
+    lib.vp8_loopfilter_apply_keyframe.argtypes = [C.POINTER(vp8g.Yuv420Image), C.POINTER(vp8g.Vp8DecodedFrame)]
+    f = vp8g.synth_frame(300, 170, seed, profile)
+    w, h = int(f.frame.mb_cols) * 16, int(f.frame.mb_rows) * 16
+    rng = np.random.default_rng(seed)
+    planes = [rng.integers(0, 256, size=n, dtype=np.uint8) for n in (w * h, w * h // 4, w * h // 4)]
+    img = vp8g.Yuv420Image()
+    assert lib.yuv420_alloc(C.byref(img), w, h) == 0
+    for dst, src in zip((img.y, img.u, img.v), planes):
+        C.memmove(dst, src.ctypes.data, src.nbytes)
+    assert lib.vp8_loopfilter_apply_keyframe(C.byref(img), C.byref(f.frame)) == 0
+    got = [np.ctypeslib.as_array(p, shape=(a.size,)).copy() for p, a in zip((img.y, img.u, img.v), planes)]
+    exp = [p.copy() for p in planes]
+    assert vp8g.oracle_lib().oracle_loopfilter(*[p.ctypes.data for p in exp], C.byref(f.frame)) == 0
+    for g, e in zip(got, exp):
+        assert np.array_equal(g, e)
+    lib.yuv420_free(C.byref(img))
+
+
+@pytest.mark.parametrize("rel", ["big/fhd_normal_sharp5.webp", "webp/" + "blockcheck2_16x16_000_000_000_255_255_255_q010.webp",
+                                 "commons/penguin-q40.webp"])
+@pytest.mark.parametrize("flag", ["-yuv", "-yuvf"])
+def test_cli_end_to_end(manifest, tmp_path, rel, flag):
+    """`decoder -yuv/-yuvf in out` (the reference's CLI contract), byte-compared like the
+    reference's gates (scripts/m6_*.sh, m7_*.sh: cmp against dwebp)."""
+    out = tmp_path / "o.i420"
+    r = subprocess.run([str(ROOT / "webp-decoder_amd/bin/decoder"), flag, str(FIXTURES / rel), str(out)],
+                       capture_output=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    key = "yuvf_sha256" if flag == "-yuvf" else "yuv_sha256"
+    assert sha(out.read_bytes()) == manifest["files"][rel][key]

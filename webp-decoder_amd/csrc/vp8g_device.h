@@ -1,0 +1,46 @@
+// vp8g_device.h -- internal interface between the C-ABI shim and the gfx950 kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "vp8g.h"
+
+namespace vp8g {
+
+// Per-wave LDS scratch (bytes).  All offsets are 16-B aligned where a 16-B access is made.
+constexpr int kLfY = 0;       // luma filter tile: 20 rows x 32 cols (4 rows above + 16 MB rows;
+                              // two MB columns as a ring, slot = mb_col & 1)
+constexpr int kLfU = 640;     // chroma tiles: 12 rows x 16 cols (4 above + 8 MB rows; ring of 2)
+constexpr int kLfV = 832;
+constexpr int kAbY = 1024;    // luma above row: [15] corner P, [16..31] A, [32..35] above-right
+constexpr int kAbUV = 1072;   // chroma above rows: U P@7 A@8..15, V P@23 A@24..31
+constexpr int kLeft = 1104;   // unfiltered left columns: Y 0..15, U 16..23, V 24..31
+constexpr int kResid = 1136;  // B_PRED luma residual: 16 blocks x 16 int16
+constexpr int kEdge = 1648;   // B_PRED edge arrays of the (at most 2) sub-blocks of a step
+constexpr int kWht = 1680;    // 16 int16 luma DCs out of the inverse WHT
+constexpr int kWaveBytes = 1712;
+
+// Workgroup header: progress words (16 x u32) + B_PRED predictor table (16 modes x 16 px x u16).
+constexpr int kProgress = 0;
+constexpr int kBpTable = 64;
+constexpr int kHdrBytes = 64 + 512;
+
+// Shared per-MB-column context (one frame per workgroup).
+constexpr int kCtxRecBytes = 32;   // unfiltered bottom row: Y 16, U 8, V 8 (intra prediction)
+constexpr int kCtxLfBytes = 128;   // bottom 4 rows, filter state: Y 4x16, U 4x8, V 4x8 (loop filter)
+constexpr int kCtxBytesPerCol = kCtxRecBytes + kCtxLfBytes;
+
+constexpr int kMaxLds = 163840;
+
+inline size_t lds_bytes(int waves, uint32_t ctx_cols, bool global_ctx) {
+	return (size_t)kHdrBytes + (size_t)waves * kWaveBytes + (global_ctx ? 0 : (size_t)ctx_cols * kCtxBytesPerCol);
+}
+
+// Launch the fused recon(+LF) kernel.  `global_ctx` != nullptr selects the variant whose
+// per-column context lives in device memory (frames too wide for LDS); it must hold
+// n_frames * ctx_cols * kCtxBytesPerCol bytes.
+hipError_t launch_frames(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const Vp8gBatchArrays& arrays,
+                         uint8_t* d_out, uint32_t ctx_cols, uint32_t max_mb_rows, uint8_t* global_ctx,
+                         hipStream_t stream, uint32_t waves_hint);
+
+}  // namespace vp8g
