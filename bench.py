@@ -1,0 +1,257 @@
+#!/usr/bin/env python3
+"""Benchmark: megapixels/s of filtered I420 decode (m06 recon + m07 loop filter, `-yuvf`
+semantics) on a batch of 512 independent 3840x2160 key frames per GPU (BASELINE.json configs[3];
+configs[4] = the same per GPU, sharded over 8 GPUs).
+
+Contract (driver): `python bench.py --gpus N --steps K --warmup W`; for N > 1 it is launched by
+torch.distributed.run, one rank per GPU.  A "step" = one launch of the fused kernel over the whole
+per-GPU batch (512 frames), inputs already resident in HBM.  Timed region: barrier + sync, K
+steps, sync + barrier; the max over ranks is taken; value = all frames of all ranks x 8.2944 MP /
+that time.  Rank 0 prints one JSON line.
+
+Inputs: the 4 distinct 4K libwebp-encoded fixtures (tests/fixtures/big/uhd_*.webp; normal and
+simple filter, sharpness 0-6, 1 or 4 segments) are entropy-decoded once on the host by the C11
+front end; slot i of the batch is a separate HBM copy of fixture i % 4 (512 x 26.6 MB >> the
+256 MB Infinity Cache, so no cache inflation).  Correctness: after timing, 4 slots are copied
+back and compared with the reference decoder's sha256 from tests/golden/manifest.json.
+
+roofline: the kernel is HBM-bound (8-bit integer stencils, no MFMA).  Algorithmic bytes per
+launch = MBs x 820 B (800 B int16 coefficients + 20 B side info); the achieved
+rate uses the average kernel duration measured with HIP events on the launch stream.  `traffic`
+(PMC HBM bytes) comes from the rocprofv3 FETCH_SIZE/WRITE_SIZE pass committed under profiles/
+(see DESIGN.md §5), or null when that file is absent.
+
+cpu_baseline (rank 0, N = 1 only): the reference's own m06+m07 (oracle/_ref/libref.so, compiled
+from the reference sources) when present, else our C restatement (oracle/liboracle.so), timed on
+a bounded sample of the same 4K frames with one frame per thread on 16 host threads.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import hashlib
+import json
+import os
+import pathlib
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = pathlib.Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "webp-decoder_amd"))
+import vp8g  # noqa: E402
+
+FIXTURES = [
+    "big/uhd_a_normal_seg4.webp",
+    "big/uhd_b_simple_sharp3.webp",
+    "big/uhd_c_normal_sharp6_seg1.webp",
+    "big/uhd_d_normal_q90.webp",
+]
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+TRAFFIC_FILE = ROOT / "profiles" / "traffic_4k_batch.json"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=512, help="frames per GPU (config 4: 512)")
+    ap.add_argument("--unfiltered", action="store_true", help="-yuv semantics (m06 only)")
+    ap.add_argument("--waves", type=int, default=0, help="waves per frame workgroup (0 = default)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
+    return ap.parse_args()
+
+
+class Batch:
+    """Device-resident batch: the nine Vp8DecodedFrame arrays concatenated over frames."""
+
+    def __init__(self, frames: list, n: int, filtered: bool, dev: torch.device):
+        self.n = n
+        mbs = [f.mb_total for f in frames]
+        self.mb_per = mbs[0]
+        assert all(m == self.mb_per for m in mbs)
+        total = n * self.mb_per
+        self.total_mb = total
+        self.arrays = {}
+        for name, dt, per in vp8g.FRAME_ARRAYS:
+            if name == "skip_coeff":
+                continue
+            tdt = torch.int16 if dt == np.int16 else torch.uint8
+            t = torch.empty(total * per, dtype=tdt, device=dev)
+            view = t.view(n, self.mb_per * per)
+            for k, f in enumerate(frames):
+                src = torch.from_numpy(f.array(name).copy()).to(dev)
+                view[k::len(frames)] = src  # slot i <- fixture i % K (separate HBM copies)
+                del src
+            self.arrays[name] = t
+        self.frame_bytes = (vp8g.i420_size(frames[0].width, frames[0].height) + 255) // 256 * 256
+        self.out = torch.empty(n * self.frame_bytes, dtype=torch.uint8, device=dev)
+        self.status = torch.zeros(4, dtype=torch.int32, device=dev)
+        descs = (vp8g.Vp8gFrameDesc * n)()
+        for i in range(n):
+            descs[i] = vp8g.make_desc(frames[i % len(frames)], filtered, i * self.mb_per, i * self.frame_bytes)
+        self.h_descs = descs
+        self.d_descs = torch.frombuffer(bytearray(bytes(descs)), dtype=torch.uint8).to(dev)
+        a = vp8g.Vp8gBatchArrays()
+        for name in ("coeff_y", "coeff_u", "coeff_v", "coeff_y2", "ymode", "uv_mode", "segment_id", "has_coeff", "bmode"):
+            setattr(a, name, self.arrays[name].data_ptr())
+        a.src = None
+        a.status = self.status.data_ptr()
+        self.c_arrays = a
+
+    def launch(self, stream, waves: int):
+        rc = vp8g.gpu_lib().vp8g_decode_batch_device(self.h_descs, C.c_void_p(self.d_descs.data_ptr()), self.n,
+                                                      C.byref(self.c_arrays), C.c_void_p(self.out.data_ptr()),
+                                                      C.c_void_p(stream), waves)
+        if rc != 0:
+            raise RuntimeError(f"launch failed: {vp8g.gpu_lib().vp8g_last_error()!r}")
+
+    def frame_output(self, i: int, w: int, h: int) -> bytes:
+        o = i * self.frame_bytes
+        return self.out[o:o + vp8g.i420_size(w, h)].cpu().numpy().tobytes()
+
+
+def cpu_baseline(frames, filtered, threads, seconds):
+    kind = "reference" if vp8g.ref_available() else "port"
+    # calibrate on one frame per thread, then size the sample for ~`seconds` of wall time
+    t = vp8g.cpu_time_batch(frames, threads, threads, filtered, kind)
+    if t <= 0:
+        return None
+    per = t / threads
+    n = max(threads, int(seconds / per) // threads * threads)
+    t = vp8g.cpu_time_batch(frames, n, threads, filtered, kind)
+    if t <= 0:
+        return None
+    mp = n * frames[0].width * frames[0].height / 1e6
+    return {"value": round(mp / t, 2), "unit": "MP/s", "cores": threads, "kind": kind,
+            "sample": f"{n} x 3840x2160 frames (the 4 bench fixtures round-robin), one frame per thread, "
+                      f"{'recon+LF (-yuvf)' if filtered else 'recon (-yuv)'} on pre-decoded input, {t:.1f} s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    filtered = not args.unfiltered
+
+    manifest = json.loads((ROOT / "tests" / "golden" / "manifest.json").read_text())
+    frames = [vp8g.decode_file(ROOT / "tests" / "fixtures" / r) for r in FIXTURES]
+    W, H = frames[0].width, frames[0].height
+    batch = Batch(frames, args.frames, filtered, dev)
+    if dist is not None:
+        # per-frame parameter blocks (dequant + loop-filter tables) are shared: rank 0's go to all
+        dist.broadcast(batch.d_descs, src=0)
+    stream = torch.cuda.current_stream(dev)
+
+    for _ in range(args.warmup):
+        batch.launch(stream.cuda_stream, args.waves)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    lib = vp8g.gpu_lib()
+    stamps = hasattr(lib, "vp8g_debug_stamps")  # diagnostic build (VP8G_STAMPS) only
+    if stamps:
+        zero = (C.c_ulonglong * 16)()
+        lib.vp8g_debug_stamps(zero, 1)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        evs[s][0].record(stream)
+        batch.launch(stream.cuda_stream, args.waves)
+        evs[s][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    if int(batch.status[0].item()) != 0:
+        raise RuntimeError("kernel reported a dependency-wait timeout")
+
+    # parity spot check: 4 slots (one per fixture) vs the reference decoder's hashes
+    key = "yuvf_sha256" if filtered else "yuv_sha256"
+    ok = all(hashlib.sha256(batch.frame_output(i, W, H)).hexdigest() == manifest["files"][FIXTURES[i % 4]][key]
+             for i in range(min(4, args.frames)))
+    if dist is not None:
+        t = torch.tensor([elapsed, kern_ms, float(ok)], dtype=torch.float64, device=dev)
+        tmax = t.clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tmin = t.clone()
+        dist.all_reduce(tmin, op=dist.ReduceOp.MIN)
+        elapsed, kern_ms, ok = float(tmax[0]), float(tmax[1]), bool(tmin[2] > 0.5)
+
+    total_frames = args.frames * world
+    mp = total_frames * W * H / 1e6
+    value = mp * args.steps / elapsed
+    ms_per_step = elapsed * 1e3 / args.steps
+    bytes_read = batch.total_mb * vp8g.BYTES_READ_PER_MB
+    achieved = bytes_read / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    if TRAFFIC_FILE.exists():
+        tj = json.loads(TRAFFIC_FILE.read_text())
+        if tj.get("frames") == args.frames and tj.get("filtered") == filtered:
+            traffic = tj.get("hbm_bytes_per_launch")
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(frames, filtered, args.cpu_threads, args.cpu_seconds)
+
+    stamp_shares = None
+    if stamps:
+        acc = (C.c_ulonglong * 16)()
+        lib.vp8g_debug_stamps(acc, 1)
+        tot = sum(acc[:8]) or 1
+        names = ["residual+loads", "dep_wait", "borders", "recon", "save_ctx", "loopfilter", "store", "publish"]
+        stamp_shares = {n: round(acc[i] / tot, 4) for i, n in enumerate(names)}
+        stamp_shares["cycles_per_mb_per_wave"] = round(tot / (batch.total_mb * args.steps), 1)
+    if rank == 0:
+        line = {
+            "metric": "megapixels/sec filtered I420 decode (4K keyframe batch)" if filtered else
+                      "megapixels/sec unfiltered I420 decode (4K keyframe batch)",
+            "value": round(value, 1),
+            "unit": "MP/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "4 libwebp-encoded 3840x2160 fixtures, host-entropy-decoded once, replicated to "
+                    f"{args.frames} HBM slots per GPU (synthetic batch of real frames)",
+            "config": {"workload": f"{args.frames} x 3840x2160 keyframes per GPU, recon+loop filter (-yuvf), "
+                                   "inputs device-resident" if filtered else
+                                   f"{args.frames} x 3840x2160 keyframes per GPU, recon only (-yuv)",
+                       "frames_per_gpu": args.frames, "width": W, "height": H,
+                       "parallelism": f"dp{world} (independent frames, no data-path collective)"},
+            "parity": "bit-exact vs reference (4 slots sha256)" if ok else "MISMATCH",
+            "kernel_ms_per_step": round(kern_ms, 3),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
+                         "algorithmic_bytes_per_launch": bytes_read},
+            "cpu_baseline": cpu,
+        }
+        if stamp_shares:
+            line["stamps"] = stamp_shares
+        print(json.dumps(line), flush=True)
+    for f in frames:
+        f.free()
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -25,6 +25,26 @@
 
 #define DEV __device__ __forceinline__
 
+// Diagnostic builds only (never in the shipped library): VP8G_STAMPS accumulates per-phase
+// shader-clock cycles (s_memtime) into g_vp8g_stamps; VP8G_ABLATE skips phases (timing only,
+// output wrong): 1 = loop filter, 2 = B_PRED steps, 4 = pixel stores, 8 = dependency wait.
+#ifndef VP8G_ABLATE
+#define VP8G_ABLATE 0
+#endif
+#ifdef VP8G_STAMPS
+__device__ unsigned long long g_vp8g_stamps[16];
+#define STAMP(i)                                                  \
+	do {                                                          \
+		const uint64_t t_ = __builtin_amdgcn_s_memtime();         \
+		st_acc[i] += t_ - st_prev;                                \
+		st_prev = t_;                                             \
+	} while (0)
+#else
+#define STAMP(i) \
+	do {         \
+	} while (0)
+#endif
+
 namespace vp8g {
 namespace {
 
@@ -248,6 +268,10 @@ __global__ __launch_bounds__(NW * 64) void frame_kernel(const Vp8gFrameDesc* __r
 		return (const u32x4*)(A.coeff_y2 + m * 16 + (ln - 48) * 8);
 	};
 
+#ifdef VP8G_STAMPS
+	uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+	uint64_t st_prev = __builtin_amdgcn_s_memtime();
+#endif
 	for (uint32_t r = (uint32_t)wave; r < R; r += NW) {
 		const uint32_t y0 = r * 16, cy0 = r * 8;
 		u32x4 nxt = {0u, 0u, 0u, 0u};
@@ -372,8 +396,9 @@ __global__ __launch_bounds__(NW * 64) void frame_kernel(const Vp8gFrameDesc* __r
 				}
 			}
 
+			STAMP(0);
 			// ------------------------------------------------ wait for MB(r-1, c+1)
-			if (r > 0) {
+			if (r > 0 && !(VP8G_ABLATE & 8)) {
 				const uint32_t need = (r - 1) * C + ((c + 2 < C) ? c + 2 : C);
 				const uint32_t pw = (uint32_t)((wave + NW - 1) % NW);
 				uint32_t spins = 0;
@@ -392,6 +417,7 @@ __global__ __launch_bounds__(NW * 64) void frame_kernel(const Vp8gFrameDesc* __r
 				asm volatile("" ::: "memory");
 			}
 
+			STAMP(1);
 			// ------------------------------------------------ borders + loop-filter top strip
 			if (!lf_only) {
 				const bool top = r == 0;
@@ -431,6 +457,7 @@ __global__ __launch_bounds__(NW * 64) void frame_kernel(const Vp8gFrameDesc* __r
 			}
 			wave_lds_sync();
 
+			STAMP(2);
 			// ------------------------------------------------ prediction + reconstruction
 			if (lf_only) {
 				// loop-filter-only mode: the MB's pixels come from the padded input image
@@ -491,7 +518,7 @@ __global__ __launch_bounds__(NW * 64) void frame_kernel(const Vp8gFrameDesc* __r
 						}
 					}
 				}
-				if (bpred) {
+				if (bpred && !(VP8G_ABLATE & 2)) {
 					// B_PRED: 16 sub-blocks along the 2i+j wavefront (10 steps, <= 2 sub-blocks
 					// each), using already reconstructed pixels (reference vp8_recon.c:454-530)
 					int16_t* rs = (int16_t*)(wv + kResid);
@@ -563,6 +590,7 @@ __global__ __launch_bounds__(NW * 64) void frame_kernel(const Vp8gFrameDesc* __r
 			}
 			wave_lds_sync();
 
+			STAMP(3);
 			// ------------------------------------------------ save unfiltered context
 			if (!lf_only) {
 				if (lane < 4) {  // bottom rows -> ctx_rec[c] for the next MB row
@@ -586,8 +614,9 @@ __global__ __launch_bounds__(NW * 64) void frame_kernel(const Vp8gFrameDesc* __r
 			}
 			wave_lds_sync();
 
+			STAMP(4);
 			// ------------------------------------------------ loop filter MB(r, c)
-			if (lf_on) {
+			if (lf_on && !(VP8G_ABLATE & 1)) {
 				const uint8_t* lp = D.lf[seg][bpred ? 1 : 0];
 				const int E = lp[0], I = lp[1], T = lp[2];
 				if (E != 0) {
@@ -659,11 +688,12 @@ __global__ __launch_bounds__(NW * 64) void frame_kernel(const Vp8gFrameDesc* __r
 				}
 			}
 
+			STAMP(5);
 			// ------------------------------------------------ store final pixels
 			// 8-byte chunk store with crop; falls back to bytes at the right edge / misalignment
 			auto put8 = [&](uint8_t* plane, uint32_t stride, uint32_t vis_w, uint32_t vis_h, uint32_t row, uint32_t col,
 			                uint2 v) {
-				if (row >= vis_h || col >= vis_w) return;
+				if (row >= vis_h || col >= vis_w || (VP8G_ABLATE & 4)) return;
 				uint8_t* d = plane + (size_t)row * stride + col;
 				const uint32_t n = vis_w - col;
 				if (n >= 8 && (((uintptr_t)d) & 7) == 0) {
@@ -729,12 +759,18 @@ __global__ __launch_bounds__(NW * 64) void frame_kernel(const Vp8gFrameDesc* __r
 			}
 			wave_lds_sync();
 
+			STAMP(6);
 			// ------------------------------------------------ publish progress
 			ctx.publish_fence();
 			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 			if (lane == 0) __hip_atomic_store(prog + wave, r * C + c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+			STAMP(7);
 		}
 	}
+#ifdef VP8G_STAMPS
+	if (lane0 == 0)
+		for (int i = 0; i < 8; i++) atomicAdd(&g_vp8g_stamps[i], (unsigned long long)st_acc[i]);
+#endif
 }
 
 template <int NW, bool kG>
@@ -751,6 +787,17 @@ hipError_t launch_t(const Vp8gFrameDesc* d_descs, uint32_t n, const Vp8gBatchArr
 }
 
 }  // namespace
+
+#ifdef VP8G_STAMPS
+extern "C" __attribute__((visibility("default"))) int vp8g_debug_stamps(unsigned long long* out, int reset) {
+	if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vp8g_stamps), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+	if (reset) {
+		unsigned long long z[16] = {0};
+		if (hipMemcpyToSymbol(HIP_SYMBOL(g_vp8g_stamps), z, sizeof(z)) != hipSuccess) return -1;
+	}
+	return 0;
+}
+#endif
 
 hipError_t launch_frames(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const Vp8gBatchArrays& arrays,
                          uint8_t* d_out, uint32_t ctx_cols, uint32_t max_mb_rows, uint8_t* global_ctx,

@@ -156,7 +156,7 @@ def host_lib():
 
 def gpu_lib():
     """libvp8g.so: the product path.  Raises if it is not built."""
-    lib = _load("gpu", LIB_DIR / "libvp8g.so")
+    lib = _load("gpu", pathlib.Path(os.environ.get("VP8G_LIB", LIB_DIR / "libvp8g.so")))
     if not getattr(lib, "_typed", False):
         P = C.POINTER
         lib.vp8_reconstruct_keyframe_yuv.argtypes = [P(Vp8KeyFrameHeader), P(Vp8DecodedFrame), P(Yuv420Image)]
