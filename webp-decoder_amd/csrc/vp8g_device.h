@@ -7,7 +7,8 @@
 
 namespace vp8g {
 
-// Per-wave LDS scratch (bytes).  All offsets are 16-B aligned where a 16-B access is made.
+// Per-half-wave LDS scratch (bytes).  A wave works on two macroblocks at once, one per 32-lane
+// half; each half owns one of these areas.  16-B aligned where a 16-B access is made.
 constexpr int kLfY = 0;       // luma filter tile: 20 rows x 32 cols (4 rows above + 16 MB rows;
                               // two MB columns as a ring, slot = mb_col & 1)
 constexpr int kLfU = 640;     // chroma tiles: 12 rows x 16 cols (4 above + 8 MB rows; ring of 2)
@@ -15,15 +16,19 @@ constexpr int kLfV = 832;
 constexpr int kAbY = 1024;    // luma above row: [15] corner P, [16..31] A, [32..35] above-right
 constexpr int kAbUV = 1072;   // chroma above rows: U P@7 A@8..15, V P@23 A@24..31
 constexpr int kLeft = 1104;   // unfiltered left columns: Y 0..15, U 16..23, V 24..31
-constexpr int kResid = 1136;  // B_PRED luma residual: 16 blocks x 16 int16
-constexpr int kEdge = 1648;   // B_PRED edge arrays of the (at most 2) sub-blocks of a step
-constexpr int kWht = 1680;    // 16 int16 luma DCs out of the inverse WHT
-constexpr int kWaveBytes = 1712;
+constexpr int kResid = 1136;  // residual of the MB: 25 blocks (16 Y, 4 U, 4 V, Y2 slot) x 16 int16
+constexpr int kEdge = 1936;   // B_PRED edge arrays of the (at most 2) sub-blocks of a step
+constexpr int kWht = 1968;    // 16 int16 luma DCs out of the inverse WHT
+constexpr int kHalfBytes = 2000;
+constexpr int kWaveBytes = 2 * kHalfBytes;
 
-// Workgroup header: progress words (16 x u32) + B_PRED predictor table (16 modes x 16 px x u16).
-constexpr int kProgress = 0;
-constexpr int kBpTable = 64;
-constexpr int kHdrBytes = 64 + 512;
+// Workgroup header.
+constexpr int kProgress = 0;    // 16 x u32 progress words (one per wave)
+constexpr int kBpTable = 64;    // B_PRED predictor table: 16 modes x 16 px x u16
+constexpr int kDqTable = 576;   // 4 segments x 6 int16 dequant factors of this frame
+constexpr int kLfTable = 624;   // 4 segments x 2 (B_PRED?) x {E, I, T, 0}
+constexpr int kFlushTable = 656;  // 3 rounds x 32 lanes x u16 store tasks
+constexpr int kHdrBytes = 848;
 
 // Shared per-MB-column context (one frame per workgroup).
 constexpr int kCtxRecBytes = 32;   // unfiltered bottom row: Y 16, U 8, V 8 (intra prediction)
@@ -42,5 +47,8 @@ inline size_t lds_bytes(int waves, uint32_t ctx_cols, bool global_ctx) {
 hipError_t launch_frames(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const Vp8gBatchArrays& arrays,
                          uint8_t* d_out, uint32_t ctx_cols, uint32_t max_mb_rows, uint8_t* global_ctx,
                          hipStream_t stream, uint32_t waves_hint);
+
+// Waves per workgroup the launcher would use for this batch (for LDS sizing decisions).
+uint32_t pick_waves(uint32_t waves_hint, uint32_t max_mb_rows);
 
 }  // namespace vp8g

@@ -2,23 +2,28 @@
 //
 // Replaces the reference hot path src/m06_recon/vp8_recon.c:423-712 (per-MB dequant, iWHT,
 // iDCT, intra prediction, reconstruction, crop) and src/m07_loopfilter/vp8_loopfilter.c:201-283
-// (raster-order in-place deblocking), bit-exactly.
+// (raster-order in-place deblocking), bit-exactly.  Design notes: DESIGN.md §3.
 //
-// Schedule (DESIGN.md §3):
-//   * one workgroup = one frame; NW waves; wave w owns MB rows r = w, w+NW, ...
-//   * MB(r,c) needs MB(r,c-1) and MB(r-1,c+1) done, for prediction AND for the loop filter
-//     (SURVEY.md App. B), so each wave waits on an LDS progress word of the row above
-//     (value r*C + cols_done, monotone within a frame) and publishes its own after every MB;
-//   * the MB is reconstructed into a per-wave LDS tile and loop-filtered right away; the
-//     unfiltered bottom row / right column needed for intra prediction are saved before
-//     filtering (ctx_rec in the shared per-column context, kLeft per wave), and the bottom 4
-//     filtered rows that the next MB row's top-edge filter still modifies travel through
-//     ctx_lf.  Pixels are stored to HBM exactly once, when final: rows 0..11 of MB(r,c-1) after
-//     LF(r,c), rows 12..15 after LF(r+1,c-1) by the wave below.
-//   * residual work (dequant, iWHT, iDCT) depends on nothing spatial and runs before the
-//     dependency wait; the next MB's coefficients are prefetched one MB ahead.
-// Lane roles per MB: lanes 0..31 hold luma block b = lane/2 (rows 2h, 2h+1, h = lane&1) as
-// loaded by one coalesced 16-B load per lane; 32..39 U, 40..47 V, 48..49 the Y2 block.
+// Schedule:
+//   * one workgroup = one frame; NW waves; wave w owns MB row PAIRS k = w, w+NW, ...;
+//   * a wave works on two macroblocks at once: lanes 0..31 on MB(2k, t), lanes 32..63 on
+//     MB(2k+1, t-2) at step t -- the 2-column skew is exactly the VP8 dependency (MB(r,c) needs
+//     MB(r,c-1) and MB(r-1,c+1), for intra prediction AND for the raster-order loop filter,
+//     SURVEY.md App. B), so the lower half's inputs were finished by the upper half one step
+//     earlier in the same wave;
+//   * between waves: an LDS progress word per wave (pair*(C+2) + steps done, monotone); the
+//     upper half of pair k needs pair k-1's lower half 2 columns ahead of it;
+//   * each half reconstructs its MB into a per-half LDS tile and loop-filters it right away;
+//     the unfiltered bottom row / right column needed for prediction are saved first (ctx_rec,
+//     per column, shared; kLeft, per half) and the bottom 4 rows the next row's top-edge
+//     filter still modifies travel through ctx_lf.  Pixels go to HBM once, when final.
+// Lane roles inside a half (ln = lane & 31):
+//   residual: ln 0..15 = luma block ln, 16..19 = U blocks, 20..23 = V blocks, 24 = Y2; one
+//             lane holds a whole 4x4 block (two 16-B loads) and transforms it in registers;
+//   loop filter: ln 0..15 = luma rows (V-pass) / columns (H-pass), 16..23 U, 24..31 V;
+//   B_PRED: 16 lanes per sub-block, two sub-blocks per step of the 2i+j wavefront.
+// All per-pixel arithmetic is branch-free (selects, v_med3, v_sad); the only divergent
+// control flow is lane-role selection of addresses.
 #include <stdint.h>
 
 #include "vp8g_device.h"
@@ -33,11 +38,12 @@
 #endif
 #ifdef VP8G_STAMPS
 __device__ unsigned long long g_vp8g_stamps[16];
-#define STAMP(i)                                                  \
-	do {                                                          \
-		const uint64_t t_ = __builtin_amdgcn_s_memtime();         \
-		st_acc[i] += t_ - st_prev;                                \
-		st_prev = t_;                                             \
+__device__ unsigned long long g_vp8g_wave_times[64];  // frame 0: per wave {start, end} s_memrealtime
+#define STAMP(i)                                          \
+	do {                                                  \
+		const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+		st_acc[i] += t_ - st_prev;                        \
+		st_prev = t_;                                     \
 	} while (0)
 #else
 #define STAMP(i) \
@@ -47,6 +53,9 @@ __device__ unsigned long long g_vp8g_stamps[16];
 
 namespace vp8g {
 namespace {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 // ---------------------------------------------------------------------------------------------
 // B_PRED predictor table (RFC 6386 12.3; reference vp8_recon.c:218-358).  Edge array bytes in
@@ -76,10 +85,10 @@ constexpr BpTab make_bptab() {
 	                         A2(1, 0), A3(1, 0, 0), CP(0), CP(0), CP(0), CP(0), CP(0), CP(0)};
 	for (int p = 0; p < 16; p++) {
 		const int r = p >> 2, c = p & 3;
-		t.v[2 * 16 + p] = A3(4 + c, 5 + c, 6 + c);                                                  // B_VE
-		t.v[3 * 16 + p] = r == 3 ? A3(1, 0, 0) : A3(4 - r, 3 - r, 2 - r);                           // B_HE
-		t.v[4 * 16 + p] = A3(5 + r + c, 6 + r + c, (7 + r + c) > 12 ? 12 : (7 + r + c));            // B_LD
-		t.v[5 * 16 + p] = A3(3 - r + c, 4 - r + c, 5 - r + c);                                      // B_RD
+		t.v[2 * 16 + p] = A3(4 + c, 5 + c, 6 + c);                                        // B_VE
+		t.v[3 * 16 + p] = r == 3 ? A3(1, 0, 0) : A3(4 - r, 3 - r, 2 - r);                 // B_HE
+		t.v[4 * 16 + p] = A3(5 + r + c, 6 + r + c, (7 + r + c) > 12 ? 12 : (7 + r + c));  // B_LD
+		t.v[5 * 16 + p] = A3(3 - r + c, 4 - r + c, 5 - r + c);                            // B_RD
 		t.v[6 * 16 + p] = vr[p];
 		t.v[7 * 16 + p] = vl[p];
 		t.v[8 * 16 + p] = hd[p];
@@ -90,6 +99,46 @@ constexpr BpTab make_bptab() {
 __constant__ BpTab kBpTab = make_bptab();
 
 // ---------------------------------------------------------------------------------------------
+// Store tasks of the loop-filter flush, per (round, lane-in-half).  Entry: bit15 valid,
+// [9:8] plane (0 Y, 1 U, 2 V), [7:6] kind (0 = top strip = the MB above's rows 12..15 (Y) /
+// 4..7 (UV), final now; 1 = body rows 0..11 / 0..3, final once this MB's left edge ran;
+// 2 = tail rows 12..15 / 4..7, handed to the row below through ctx_lf), bit5 which MB (0 cur,
+// 1 the previous column), [3:0] row within the group.
+// ---------------------------------------------------------------------------------------------
+struct FlushTab {
+	uint16_t v[96];
+};
+constexpr uint16_t FT(int plane, int kind, int prev, int k) {
+	return (uint16_t)(0x8000 | (plane << 8) | (kind << 6) | (prev << 5) | k);
+}
+constexpr FlushTab make_flushtab() {
+	FlushTab t{};
+	for (int ln = 0; ln < 32; ln++) {
+		uint16_t e0 = 0, e1 = 0, e2 = 0;
+		if (ln < 4) e0 = FT(0, 0, 0, ln);
+		else if (ln < 16) e0 = FT(0, 1, 1, ln - 4);
+		else if (ln < 20) e0 = FT(0, 2, 1, ln - 16);
+		else if (ln < 24) e0 = FT(1, 0, 0, ln - 20);
+		else if (ln < 28) e0 = FT(2, 0, 0, ln - 24);
+		else e0 = FT(1, 1, 1, ln - 28);
+		if (ln < 4) e1 = FT(2, 1, 1, ln);
+		else if (ln < 8) e1 = FT(1, 2, 1, ln - 4);
+		else if (ln < 12) e1 = FT(2, 2, 1, ln - 8);
+		else if (ln < 24) e1 = FT(0, 1, 0, ln - 12);
+		else if (ln < 28) e1 = FT(0, 2, 0, ln - 24);
+		else e1 = FT(1, 1, 0, ln - 28);
+		if (ln < 4) e2 = FT(2, 1, 0, ln);
+		else if (ln < 8) e2 = FT(1, 2, 0, ln - 4);
+		else if (ln < 12) e2 = FT(2, 2, 0, ln - 8);
+		t.v[ln] = e0;
+		t.v[32 + ln] = e1;
+		t.v[64 + ln] = e2;
+	}
+	return t;
+}
+__constant__ FlushTab kFlushTab = make_flushtab();
+
+// ---------------------------------------------------------------------------------------------
 // small helpers
 // ---------------------------------------------------------------------------------------------
 // Intra-wave LDS ordering: a wave's LDS instructions execute in issue order, so only the
@@ -97,45 +146,58 @@ __constant__ BpTab kBpTab = make_bptab();
 DEV void wave_lds_sync() { asm volatile("" ::: "memory"); }
 
 DEV int sx16(int x) { return (int)(int16_t)x; }
-DEV int sat8(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
-DEV int sclamp(int v) { return v < -128 ? -128 : (v > 127 ? 127 : v); }
-DEV int iabs(int v) { return v < 0 ? -v : v; }
-DEV int mul_s(int x) { return (x * 35468) >> 16; }          // x*sqrt(2)*sin(pi/8), RFC 14.4
-DEV int mul_c(int x) { return x + ((x * 20091) >> 16); }    // x*sqrt(2)*cos(pi/8)
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-
+DEV int sat8(int v) { return min(max(v, 0), 255); }  // v_med3_i32
+DEV int sclamp(int v) { return min(max(v, -128), 127); }
+DEV int ad(int a, int b) { return (int)__builtin_amdgcn_sad_u16((uint32_t)a, (uint32_t)b, 0u); }  // |a-b| for 0 <= a,b < 65536
+DEV int max3i(int a, int b, int c) { return max(a, max(b, c)); }
+DEV int mul_s(int x) { return (x * 35468) >> 16; }        // x*sqrt(2)*sin(pi/8), RFC 14.4
+DEV int mul_c(int x) { return x + ((x * 20091) >> 16); }  // x*sqrt(2)*cos(pi/8)
 DEV uint32_t bsum4(uint32_t w) { return __builtin_amdgcn_sad_u8(w, 0u, 0u); }
-DEV int partner(int v) { return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false); }  // lane ^ 1
-DEV uint32_t u8(const uint8_t* p) { return *p; }
 DEV uint32_t ld32(const uint8_t* p) { return *(const uint32_t*)p; }
 DEV void st32(uint8_t* p, uint32_t v) { *(uint32_t*)p = v; }
-DEV uint2 ld64(const uint8_t* p) { return *(const uint2*)p; }
-DEV void st64(uint8_t* p, uint2 v) { *(uint2*)p = v; }
+DEV u32x2 ld64(const uint8_t* p) { return *(const u32x2*)p; }
+DEV void st64(uint8_t* p, u32x2 v) { *(u32x2*)p = v; }
+DEV u32x4 ld128(const uint8_t* p) { return *(const u32x4*)p; }
+DEV void st128(uint8_t* p, u32x4 v) { *(u32x4*)p = v; }
 DEV uint32_t pack4(int a, int b, int c, int d) {
 	return (uint32_t)a | ((uint32_t)b << 8) | ((uint32_t)c << 16) | ((uint32_t)d << 24);
 }
 DEV int ubyte(uint32_t w, int i) { return (int)((w >> (8 * i)) & 0xFFu); }
+DEV uint32_t lo16(int a, int b) { return (uint32_t)(a & 0xFFFF) | ((uint32_t)b << 16); }
 // byte q (0..15) of a 16-byte value held in 4 dwords
-DEV int byte16(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, int q) {
-	uint32_t lo = __builtin_amdgcn_perm(d1, d0, (uint32_t)(q & 7) * 0x01010101u);
-	uint32_t hi = __builtin_amdgcn_perm(d3, d2, (uint32_t)(q & 7) * 0x01010101u);
+DEV int byte16(u32x4 d, int q) {
+	const uint32_t sel = (uint32_t)(q & 7) * 0x01010101u;
+	const uint32_t lo = __builtin_amdgcn_perm(d.y, d.x, sel);
+	const uint32_t hi = __builtin_amdgcn_perm(d.w, d.z, sel);
 	return (int)(((q & 8) ? hi : lo) & 0xFFu);
 }
+DEV int rdlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 
 // Per-frame context (unfiltered bottom rows + filter-state bottom rows per MB column), in LDS
 // or, for frames too wide for LDS, in device memory (read with L1-bypassing loads).
 template <bool kG>
 struct Ctx {
-	uint8_t* lds;  // smem + offset (kG == false)
-	uint8_t* g;    // device pointer (kG == true)
+	uint8_t* lds;
+	uint8_t* g;
 	DEV uint32_t rd(uint32_t off) const {
 		if constexpr (kG) return __hip_atomic_load((uint32_t*)(g + off), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 		else return ld32(lds + off);
 	}
-	DEV void wr(uint32_t off, uint32_t v) const {
-		if constexpr (kG) *(uint32_t*)(g + off) = v;
-		else st32(lds + off, v);
+	DEV u32x2 rd64(uint32_t off) const {
+		if constexpr (kG) return u32x2{rd(off), rd(off + 4)};
+		else return ld64(lds + off);
+	}
+	DEV u32x4 rd128(uint32_t off) const {
+		if constexpr (kG) return u32x4{rd(off), rd(off + 4), rd(off + 8), rd(off + 12)};
+		else return ld128(lds + off);
+	}
+	DEV void wr64(uint32_t off, u32x2 v) const {
+		if constexpr (kG) *(u32x2*)(g + off) = v;
+		else st64(lds + off, v);
+	}
+	DEV void wr128(uint32_t off, u32x4 v) const {
+		if constexpr (kG) *(u32x4*)(g + off) = v;
+		else st128(lds + off, v);
 	}
 	DEV void publish_fence() const {
 		if constexpr (kG) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -145,96 +207,154 @@ DEV uint32_t rec_off(uint32_t c) { return c * kCtxBytesPerCol; }
 DEV uint32_t lf_off(uint32_t c) { return c * kCtxBytesPerCol + kCtxRecBytes; }
 
 // ---------------------------------------------------------------------------------------------
-// Loop filter on a line of pixels (RFC 6386 15.2-15.4; reference vp8_loopfilter.c:24-164).
-// px[] is a 20-pixel line across the MB's edges: [0..3] = the neighbour (left or above),
-// [4..19] = this MB; edges sit at q0 = 4 (MB edge), 8, 12, 16 (sub-block edges).
+// Loop filter on a line of pixels (RFC 6386 15.2-15.4; reference vp8_loopfilter.c:24-164),
+// branch-free.  A line is 20 pixels held as 5 packed dwords: w[0] = the neighbour's last 4
+// pixels (left or above), w[1..4] = this MB; the edge at dword j has p3 p2 p1 p0 = bytes 0..3 of
+// w[j-1] and q0 q1 q2 q3 = bytes 0..3 of w[j] (j = 1: MB edge, 2..4: sub-block edges).
 // ---------------------------------------------------------------------------------------------
-template <int K>
-DEV void lf_mb_edge(int* px, bool en, int lim, int I, int T) {  // normal filter, MB edge
-	const int p3 = px[K - 4], p2 = px[K - 3], p1 = px[K - 2], p0 = px[K - 1];
-	const int q0 = px[K], q1 = px[K + 1], q2 = px[K + 2], q3 = px[K + 3];
-	const bool m = en && (iabs(p0 - q0) * 2 + (iabs(p1 - q1) >> 1) <= lim) && iabs(p3 - p2) <= I && iabs(p2 - p1) <= I &&
-	               iabs(p1 - p0) <= I && iabs(q3 - q2) <= I && iabs(q2 - q1) <= I && iabs(q1 - q0) <= I;
-	if (!m) return;
-	const bool hev = iabs(p1 - p0) > T || iabs(q1 - q0) > T;
-	const int w = sclamp(sclamp(p1 - q1) + 3 * (q0 - p0));
-	if (hev) {
-		px[K] = sat8(q0 - (sclamp(w + 4) >> 3));
-		px[K - 1] = sat8(p0 + (sclamp(w + 3) >> 3));
-	} else {
-		int a = (27 * w + 63) >> 7;
-		px[K - 1] = sat8(p0 + a);
-		px[K] = sat8(q0 - a);
-		a = (18 * w + 63) >> 7;
-		px[K - 2] = sat8(p1 + a);
-		px[K + 1] = sat8(q1 - a);
-		a = (9 * w + 63) >> 7;
-		px[K - 3] = sat8(p2 + a);
-		px[K + 2] = sat8(q2 - a);
-	}
+struct EdgePx {
+	int p3, p2, p1, p0, q0, q1, q2, q3;
+};
+DEV EdgePx unpack_edge(uint32_t wp, uint32_t wq) {
+	return EdgePx{ubyte(wp, 0), ubyte(wp, 1), ubyte(wp, 2), ubyte(wp, 3), ubyte(wq, 0), ubyte(wq, 1), ubyte(wq, 2), ubyte(wq, 3)};
+}
+// normal-filter edge mask (RFC 15.3 filter_yes + interior limits) and high-edge-variance
+DEV void edge_mask(const EdgePx& e, bool en, int lim, int I, int T, bool& m, bool& hev) {
+	const int d10 = ad(e.p1, e.p0), e10 = ad(e.q1, e.q0);
+	const int interior = max(max3i(ad(e.p3, e.p2), ad(e.p2, e.p1), d10), max3i(ad(e.q3, e.q2), ad(e.q2, e.q1), e10));
+	m = en && (ad(e.p0, e.q0) * 2 + (ad(e.p1, e.q1) >> 1) <= lim) && interior <= I;
+	hev = max(d10, e10) > T;
 }
 
-template <int K>
-DEV void lf_sub_edge(int* px, bool en, int lim, int I, int T) {  // normal filter, sub-block edge
-	const int p3 = px[K - 4], p2 = px[K - 3], p1 = px[K - 2], p0 = px[K - 1];
-	const int q0 = px[K], q1 = px[K + 1], q2 = px[K + 2], q3 = px[K + 3];
-	const bool m = en && (iabs(p0 - q0) * 2 + (iabs(p1 - q1) >> 1) <= lim) && iabs(p3 - p2) <= I && iabs(p2 - p1) <= I &&
-	               iabs(p1 - p0) <= I && iabs(q3 - q2) <= I && iabs(q2 - q1) <= I && iabs(q1 - q0) <= I;
-	if (!m) return;
-	const bool hev = iabs(p1 - p0) > T || iabs(q1 - q0) > T;
-	const int a = sclamp(3 * (q0 - p0) + (hev ? sclamp(p1 - q1) : 0));
+DEV void lf_mb_edge(uint32_t& wp, uint32_t& wq, bool en, int lim, int I, int T) {  // normal, MB edge
+	const EdgePx e = unpack_edge(wp, wq);
+	bool m, hev;
+	edge_mask(e, en, lim, I, T, m, hev);
+	const int w = sclamp(sclamp(e.p1 - e.q1) + 3 * (e.q0 - e.p0));
+	const int f1 = sclamp(w + 4) >> 3, f2 = sclamp(w + 3) >> 3;
+	const int a27 = (27 * w + 63) >> 7, a18 = (18 * w + 63) >> 7, a9 = (9 * w + 63) >> 7;
+	const bool mh = m && hev, mn = m && !hev;
+	const int np0 = mh ? sat8(e.p0 + f2) : (mn ? sat8(e.p0 + a27) : e.p0);
+	const int nq0 = mh ? sat8(e.q0 - f1) : (mn ? sat8(e.q0 - a27) : e.q0);
+	const int np1 = mn ? sat8(e.p1 + a18) : e.p1, nq1 = mn ? sat8(e.q1 - a18) : e.q1;
+	const int np2 = mn ? sat8(e.p2 + a9) : e.p2, nq2 = mn ? sat8(e.q2 - a9) : e.q2;
+	wp = pack4(e.p3, np2, np1, np0);
+	wq = pack4(nq0, nq1, nq2, e.q3);
+}
+
+DEV void lf_sub_edge(uint32_t& wp, uint32_t& wq, bool en, int lim, int I, int T) {  // normal, sub-block edge
+	const EdgePx e = unpack_edge(wp, wq);
+	bool m, hev;
+	edge_mask(e, en, lim, I, T, m, hev);
+	const int a = sclamp(3 * (e.q0 - e.p0) + (hev ? sclamp(e.p1 - e.q1) : 0));
 	const int f1 = sclamp(a + 4) >> 3, f2 = sclamp(a + 3) >> 3;
-	px[K] = sat8(q0 - f1);
-	px[K - 1] = sat8(p0 + f2);
-	if (!hev) {
-		const int a2 = (f1 + 1) >> 1;
-		px[K + 1] = sat8(q1 - a2);
-		px[K - 2] = sat8(p1 + a2);
-	}
+	const int a2 = (f1 + 1) >> 1;
+	const bool mn = m && !hev;
+	const int nq0 = m ? sat8(e.q0 - f1) : e.q0, np0 = m ? sat8(e.p0 + f2) : e.p0;
+	const int nq1 = mn ? sat8(e.q1 - a2) : e.q1, np1 = mn ? sat8(e.p1 + a2) : e.p1;
+	wp = pack4(e.p3, e.p2, np1, np0);
+	wq = pack4(nq0, nq1, e.q2, e.q3);
 }
 
-template <int K>
-DEV void lf_simple_edge(int* px, bool en, int lim) {  // simple filter (luma only)
-	const int p1 = px[K - 2], p0 = px[K - 1], q0 = px[K], q1 = px[K + 1];
-	if (!(en && iabs(p0 - q0) * 2 + (iabs(p1 - q1) >> 1) <= lim)) return;
+DEV void lf_simple_edge(uint32_t& wp, uint32_t& wq, bool en, int lim) {  // simple filter (luma only)
+	const int p1 = ubyte(wp, 2), p0 = ubyte(wp, 3), q0 = ubyte(wq, 0), q1 = ubyte(wq, 1);
+	const bool m = en && ad(p0, q0) * 2 + (ad(p1, q1) >> 1) <= lim;
 	const int a = sclamp(sclamp(p1 - q1) + 3 * (q0 - p0));
-	px[K] = sat8(q0 - (sclamp(a + 4) >> 3));
-	px[K - 1] = sat8(p0 + (sclamp(a + 3) >> 3));
+	const int nq0 = m ? sat8(q0 - (sclamp(a + 4) >> 3)) : q0, np0 = m ? sat8(p0 + (sclamp(a + 3) >> 3)) : p0;
+	wp = (wp & 0x0000FFFFu) | ((uint32_t)p1 << 16) | ((uint32_t)np0 << 24);
+	wq = (wq & 0xFFFF0000u) | (uint32_t)nq0 | ((uint32_t)q1 << 8);
 }
 
 // All edges of one line, in the reference order (MB edge, then sub-block edges).  `is_y`
-// enables the luma-only edges at 12 and 16; chroma has its single inner edge at 8.
-DEV void lf_line(int* px, bool simple, bool mb_edge, bool inner, bool is_y, int E, int I, int T) {
-	if (simple) {
-		lf_simple_edge<4>(px, mb_edge && is_y, (E + 2) * 2 + I);
-		lf_simple_edge<8>(px, inner && is_y, E * 2 + I);
-		lf_simple_edge<12>(px, inner && is_y, E * 2 + I);
-		lf_simple_edge<16>(px, inner && is_y, E * 2 + I);
+// enables the luma-only edges at dwords 3 and 4; chroma has its single inner edge at dword 2.
+template <bool kSimple>
+DEV void lf_line(uint32_t* w, bool mb_edge, bool inner, bool is_y, int E, int I, int T) {
+	if constexpr (kSimple) {
+		lf_simple_edge(w[0], w[1], mb_edge && is_y, (E + 2) * 2 + I);
+		lf_simple_edge(w[1], w[2], inner && is_y, E * 2 + I);
+		lf_simple_edge(w[2], w[3], inner && is_y, E * 2 + I);
+		lf_simple_edge(w[3], w[4], inner && is_y, E * 2 + I);
 	} else {
-		lf_mb_edge<4>(px, mb_edge, 2 * (E + 2) + I, I, T);
-		lf_sub_edge<8>(px, inner, 2 * E + I, I, T);
-		lf_sub_edge<12>(px, inner && is_y, 2 * E + I, I, T);
-		lf_sub_edge<16>(px, inner && is_y, 2 * E + I, I, T);
+		lf_mb_edge(w[0], w[1], mb_edge, 2 * (E + 2) + I, I, T);
+		lf_sub_edge(w[1], w[2], inner, 2 * E + I, I, T);
+		lf_sub_edge(w[2], w[3], inner && is_y, 2 * E + I, I, T);
+		lf_sub_edge(w[3], w[4], inner && is_y, 2 * E + I, I, T);
 	}
 }
+
+// Both passes of the loop filter over this lane's line of the MB held in LDS.
+template <bool kSimple>
+DEV void lf_mb(uint8_t* tY, uint8_t* tU, uint8_t* tV, int ln, int slot, bool en, bool mb_v, bool mb_h, bool inner, int E,
+               int I, int T) {
+	const bool isy = ln < 16;
+	// vertical edges: one line per lane along a pixel row (Y 16, U 8, V 8)
+	{
+		uint8_t* rowp = isy ? tY + (4 + ln) * 32 : (ln < 24 ? tU : tV) + (4 + (ln & 7)) * 16;
+		const int ring = isy ? 7 : 3;  // dword ring of the two-MB tile row
+		const int base = isy ? slot * 4 : slot * 2;
+		uint32_t w[5];
+#pragma unroll
+		for (int q = 0; q < 5; q++) w[q] = (q < 3 || isy) ? ld32(rowp + 4 * ((base - 1 + q) & ring)) : 0u;
+		lf_line<kSimple>(w, en && mb_v, en && inner, isy, E, I, T);
+		if (en && (isy || !kSimple)) {
+#pragma unroll
+			for (int q = 0; q < 5; q++)
+				if (q < 3 || isy) st32(rowp + 4 * ((base - 1 + q) & ring), w[q]);
+		}
+	}
+	wave_lds_sync();
+	// horizontal edges: one line per lane down a pixel column
+	{
+		uint8_t* colp = isy ? tY + slot * 16 + ln : (ln < 24 ? tU : tV) + slot * 8 + (ln & 7);
+		const int stride = isy ? 32 : 16;
+		uint32_t w[5];
+#pragma unroll
+		for (int q = 0; q < 5; q++) {
+			if (q < 3 || isy)
+				w[q] = pack4(colp[(4 * q) * stride], colp[(4 * q + 1) * stride], colp[(4 * q + 2) * stride],
+				             colp[(4 * q + 3) * stride]);
+			else w[q] = 0u;
+		}
+		lf_line<kSimple>(w, en && mb_h, en && inner, isy, E, I, T);
+		if (en && (isy || !kSimple)) {
+#pragma unroll
+			for (int q = 1; q < 19; q++)
+				if (q < 11 || isy) colp[q * stride] = (uint8_t)ubyte(w[q >> 2], q & 3);
+		}
+	}
+	wave_lds_sync();
+}
+
+// one lane's 32 bytes of coefficients (or side info) for the next step
+struct Pref {
+	u32x4 a, b;
+	uint32_t side;
+};
 
 // ---------------------------------------------------------------------------------------------
 // The fused kernel.
 // ---------------------------------------------------------------------------------------------
+// Occupancy target: two workgroups (frames) per CU -> 2*NW waves per CU.
+template <int NW>
+constexpr int min_waves_per_simd() { return NW >= 2 ? (2 * NW) / 4 : 1; }
+
 template <int NW, bool kG>
-__global__ __launch_bounds__(NW * 64) void frame_kernel(const Vp8gFrameDesc* __restrict__ descs, Vp8gBatchArrays A,
+__global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kernel(const Vp8gFrameDesc* __restrict__ descs, Vp8gBatchArrays A,
                                                         uint8_t* __restrict__ out, uint32_t ctx_cols,
                                                         uint8_t* __restrict__ gctx) {
 	extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 	const int lane0 = (int)(threadIdx.x & 63);
 	const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
 	const uint32_t f = blockIdx.x;
+	const Vp8gFrameDesc& D = descs[f];
 
 	for (int i = (int)threadIdx.x; i < 256; i += NW * 64) ((uint16_t*)(smem + kBpTable))[i] = kBpTab.v[i];
+	for (int i = (int)threadIdx.x; i < 96; i += NW * 64) ((uint16_t*)(smem + kFlushTable))[i] = kFlushTab.v[i];
+	if (threadIdx.x < 24) ((int16_t*)(smem + kDqTable))[threadIdx.x] = D.dq[threadIdx.x / 6][threadIdx.x % 6];
+	if (threadIdx.x < 32) smem[kLfTable + threadIdx.x] = D.lf[threadIdx.x >> 3][(threadIdx.x >> 2) & 1][threadIdx.x & 3];
 	if (threadIdx.x < 16) ((uint32_t*)(smem + kProgress))[threadIdx.x] = 0;
 	__syncthreads();
 
-	const Vp8gFrameDesc& D = descs[f];
 	const uint32_t C = D.mb_cols, R = D.mb_rows;
 	const uint32_t flags = D.flags;
 	const bool lf_on = (flags & VP8G_F_LOOPFILTER) != 0;
@@ -246,160 +366,169 @@ __global__ __launch_bounds__(NW * 64) void frame_kernel(const Vp8gFrameDesc* __r
 	uint8_t* const outV = out + D.out_v;
 	const uint32_t W = D.width, H = D.height, CW = (D.width + 1) >> 1, CH = (D.height + 1) >> 1;
 	const uint32_t sy = D.stride_y, suv = D.stride_uv;
-
-	uint8_t* const wv = smem + kHdrBytes + wave * kWaveBytes;
-	uint8_t* const tY = wv + kLfY;
-	uint8_t* const tU = wv + kLfU;
-	uint8_t* const tV = wv + kLfV;
-	uint8_t* const abY = wv + kAbY;
-	uint8_t* const abUV = wv + kAbUV;
-	uint8_t* const left = wv + kLeft;
 	uint32_t* const prog = (uint32_t*)(smem + kProgress);
-	const uint16_t* const bptab = (const uint16_t*)(smem + kBpTable);
 	Ctx<kG> ctx;
 	ctx.lds = smem + kHdrBytes + NW * kWaveBytes;
 	ctx.g = kG ? gctx + (size_t)f * ctx_cols * kCtxBytesPerCol : nullptr;
-
-	// coefficient source of a lane: 16 bytes = 8 int16 (two rows of one 4x4 block)
-	auto coeff_ptr = [&](int ln, uint64_t m) -> const u32x4* {
-		if (ln < 32) return (const u32x4*)(A.coeff_y + m * 256 + ln * 8);
-		if (ln < 40) return (const u32x4*)(A.coeff_u + m * 64 + (ln - 32) * 8);
-		if (ln < 48) return (const u32x4*)(A.coeff_v + m * 64 + (ln - 40) * 8);
-		return (const u32x4*)(A.coeff_y2 + m * 16 + (ln - 48) * 8);
-	};
+	const uint32_t npairs = (R + 1) >> 1;
+	const uint32_t CP2 = C + 2;
 
 #ifdef VP8G_STAMPS
 	uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 	uint64_t st_prev = __builtin_amdgcn_s_memtime();
+	if (f == 0 && lane0 == 0 && wave < 32) g_vp8g_wave_times[2 * wave] = __builtin_amdgcn_s_memrealtime();
 #endif
-	for (uint32_t r = (uint32_t)wave; r < R; r += NW) {
-		const uint32_t y0 = r * 16, cy0 = r * 8;
-		u32x4 nxt = {0u, 0u, 0u, 0u};
-		if (lane0 < 50 && !lf_only) nxt = __builtin_nontemporal_load(coeff_ptr(lane0, mb0 + (uint64_t)r * C));
 
-		for (uint32_t c = 0; c < C; c++) {
-			const uint64_t m = mb0 + (uint64_t)r * C + c;
-			// Lane-derived values are recomputed every MB from a laundered lane id: hoisting the
-			// ~100 lane-dependent LDS addresses out of the loop would exhaust the VGPR budget.
+	// Loads for one lane of one step: coefficient blocks (ln 0..24), bmode (25), side bytes (26..29).
+	auto prefetch = [&](int lane, uint32_t rA, bool two, int tt) -> Pref {
+		Pref p;
+		p.a = u32x4{0u, 0u, 0u, 0u};
+		p.b = p.a;
+		p.side = 0;
+		const int hh = lane >> 5, ln = lane & 31;
+		const int cn = tt - 2 * hh;
+		if ((hh == 0 || two) && cn >= 0 && cn < (int)C) {
+			const uint64_t m = mb0 + (uint64_t)(rA + hh) * C + (uint32_t)cn;
+			if (ln < 25) {
+				const int16_t* src = ln < 16 ? A.coeff_y + (m * 16 + ln) * 16
+				                             : (ln < 20 ? A.coeff_u + (m * 4 + ln - 16) * 16
+				                                        : (ln < 24 ? A.coeff_v + (m * 4 + ln - 20) * 16 : A.coeff_y2 + m * 16));
+				if (!lf_only) {
+					p.a = __builtin_nontemporal_load((const u32x4*)src);
+					p.b = __builtin_nontemporal_load((const u32x4*)src + 1);
+				}
+			} else if (ln == 25) {
+				if (!lf_only) p.a = *(const u32x4*)(A.bmode + m * 16);
+			} else if (ln < 30) {
+				const uint8_t* sp = ln == 26 ? A.ymode : (ln == 27 ? A.uv_mode : (ln == 28 ? A.segment_id : A.has_coeff));
+				p.side = sp[m];
+			}
+		}
+		return p;
+	};
+
+	for (uint32_t k = (uint32_t)wave; k < npairs; k += NW) {
+		const uint32_t rA = 2 * k;
+		const bool two = rA + 1 < R;
+		const uint32_t T = two ? CP2 : C;
+		Pref nxt = prefetch(lane0, rA, two, 0);
+
+		for (uint32_t t = 0; t < T; t++) {
+			// Lane-derived values are recomputed every step from a laundered lane id: hoisting the
+			// lane-dependent LDS addresses out of the loop would exhaust the VGPR budget.
 			int lane = lane0;
 			asm volatile("" : "+v"(lane));
-			const bool is_yl = lane < 32, is_uvl = lane >= 32 && lane < 48, is_y2l = lane == 48 || lane == 49;
-			const int h = lane & 1;
-			const int yb = lane >> 1;          // luma block (lanes 0..31)
-			const int uvk = (lane - 32) & 15;  // chroma lane index 0..15
-			const int uvp = uvk >> 3;          // 0 = U, 1 = V
-			const int uvb = (uvk & 7) >> 1;    // chroma block 0..3
-			const bool loads = lane < 50 && !lf_only;
+			const int hh = lane >> 5, ln = lane & 31;
+			const uint32_t r = rA + (uint32_t)hh;
+			const int c = (int)t - 2 * hh;
+			const bool act = (hh == 0 || two) && c >= 0 && c < (int)C;
+			const uint32_t cu = (uint32_t)c;
+			const int slot = c & 1;
+			uint8_t* const hv = smem + kHdrBytes + wave * kWaveBytes + hh * kHalfBytes;  // this half's area
+			uint8_t* const tY = hv + kLfY;
+			uint8_t* const tU = hv + kLfU;
+			uint8_t* const tV = hv + kLfV;
+			uint8_t* const abY = hv + kAbY;
+			uint8_t* const abUV = hv + kAbUV;
+			uint8_t* const left = hv + kLeft;
 
-			const u32x4 cw = nxt;
-			if (loads && c + 1 < C) nxt = __builtin_nontemporal_load(coeff_ptr(lane, m + 1));
-			const int slot = (int)(c & 1);
-			const uint32_t x0 = c * 16, cx0 = c * 8;
+			const Pref cur = nxt;
+			nxt = prefetch(lane, rA, two, (int)t + 1);
 
-			// side info (uniform)
-			const int ymode = __builtin_amdgcn_readfirstlane((int)A.ymode[m]);
-			const int uvmode = __builtin_amdgcn_readfirstlane((int)A.uv_mode[m]);
-			const int seg = __builtin_amdgcn_readfirstlane((int)A.segment_id[m]) & 3;
-			const int hasc = A.has_coeff ? __builtin_amdgcn_readfirstlane((int)A.has_coeff[m]) : 0;
+			// per-half side info (lanes 26..29 / 58..61 hold it)
+			const int ymode = hh ? rdlane((int)cur.side, 58) : rdlane((int)cur.side, 26);
+			const int uvmode = hh ? rdlane((int)cur.side, 59) : rdlane((int)cur.side, 27);
+			const int seg = (hh ? rdlane((int)cur.side, 60) : rdlane((int)cur.side, 28)) & 3;
+			const int hasc = hh ? rdlane((int)cur.side, 61) : rdlane((int)cur.side, 29);
 			const bool bpred = ymode == 4;
+			const uint32_t y0 = r * 16, cy0 = r * 8, x0 = cu * 16, cx0 = cu * 8;
 
-			// ------------------------------------------------ residual (no spatial dependency)
-			int res[8];
+			// ---------------------------------------------- residual (no spatial dependency)
+			// Computed before the dependency wait and parked in LDS (kResid, 32 B per block) so that
+			// no residual registers stay live across the wait.
 			if (!lf_only) {
-				int cf[8];
-				cf[0] = (int)(int16_t)(cw.x & 0xFFFF);
-				cf[1] = (int)(int16_t)(cw.x >> 16);
-				cf[2] = (int)(int16_t)(cw.y & 0xFFFF);
-				cf[3] = (int)(int16_t)(cw.y >> 16);
-				cf[4] = (int)(int16_t)(cw.z & 0xFFFF);
-				cf[5] = (int)(int16_t)(cw.z >> 16);
-				cf[6] = (int)(int16_t)(cw.w & 0xFFFF);
-				cf[7] = (int)(int16_t)(cw.w >> 16);
-				const int16_t* dq = D.dq[seg];
-				int fdc, fac;
-				if (is_yl) fdc = dq[0], fac = dq[1];
-				else if (is_uvl) fdc = dq[2], fac = dq[3];
-				else fdc = dq[4], fac = dq[5];
-				int v[8];
+				int res[16];
+				const int cls = ln < 16 ? 0 : (ln < 24 ? 1 : 2);  // Y1, UV, Y2 factors
+				const int16_t* dqt = (const int16_t*)(smem + kDqTable) + seg * 6 + cls * 2;
+				const int fdc = dqt[0], fac = dqt[1];
+				const uint32_t w8[8] = {cur.a.x, cur.a.y, cur.a.z, cur.a.w, cur.b.x, cur.b.y, cur.b.z, cur.b.w};
+				int v[16];
+				bool anyac = false;
 #pragma unroll
-				for (int k = 0; k < 8; k++) v[k] = sx16(cf[k] * ((k == 0 && h == 0) ? fdc : fac));
-
-				if (!bpred) {
-					// inverse WHT of the Y2 block in lanes 48/49 -> 16 luma DCs (RFC 14.3)
-					if (is_y2l) {
-						int o[8];
-#pragma unroll
-						for (int k = 0; k < 8; k++) o[k] = partner(v[k]);
-						int t[8];
+				for (int i = 0; i < 16; i++) {
+					const int cf = (int)(int16_t)((w8[i >> 1] >> (16 * (i & 1))) & 0xFFFFu);
+					v[i] = sx16(cf * (i ? fac : fdc));
+					if (i) anyac |= v[i] != 0;
+				}
+				// Y2 (non-B_PRED): inverse WHT (RFC 14.3) in the Y2 lane, 16 DCs to LDS
+				if (__ballot(act && !bpred) != 0ull) {
+					if (ln == 24 && act && !bpred) {
+						int t2[16], o[16];
 #pragma unroll
 						for (int i = 0; i < 4; i++) {
-							const int r0 = h ? o[i] : v[i], r1 = h ? o[4 + i] : v[4 + i];
-							const int r2 = h ? v[i] : o[i], r3 = h ? v[4 + i] : o[4 + i];
-							const int a1 = r0 + r3, b1 = r1 + r2, c1 = r1 - r2, d1 = r0 - r3;
-							t[i] = sx16(h ? a1 - b1 : a1 + b1);
-							t[4 + i] = sx16(h ? d1 - c1 : c1 + d1);
+							const int a1 = v[i] + v[12 + i], b1 = v[4 + i] + v[8 + i];
+							const int c1 = v[4 + i] - v[8 + i], d1 = v[i] - v[12 + i];
+							t2[i] = sx16(a1 + b1);
+							t2[4 + i] = sx16(c1 + d1);
+							t2[8 + i] = sx16(a1 - b1);
+							t2[12 + i] = sx16(d1 - c1);
 						}
-						uint32_t pk[4];
 #pragma unroll
-						for (int rr = 0; rr < 2; rr++) {
-							const int* q = t + 4 * rr;
+						for (int i = 0; i < 4; i++) {
+							const int* q = t2 + 4 * i;
 							const int a1 = q[0] + q[3], b1 = q[1] + q[2], c1 = q[1] - q[2], d1 = q[0] - q[3];
-							const int o0 = sx16((a1 + b1 + 3) >> 3), o1 = sx16((c1 + d1 + 3) >> 3);
-							const int o2 = sx16((a1 - b1 + 3) >> 3), o3 = sx16((d1 - c1 + 3) >> 3);
-							pk[2 * rr] = (uint32_t)(o0 & 0xFFFF) | ((uint32_t)o1 << 16);
-							pk[2 * rr + 1] = (uint32_t)(o2 & 0xFFFF) | ((uint32_t)o3 << 16);
+							o[4 * i + 0] = sx16((a1 + b1 + 3) >> 3);
+							o[4 * i + 1] = sx16((c1 + d1 + 3) >> 3);
+							o[4 * i + 2] = sx16((a1 - b1 + 3) >> 3);
+							o[4 * i + 3] = sx16((d1 - c1 + 3) >> 3);
 						}
-						*(uint4*)(wv + kWht + h * 16) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+						st128(hv + kWht, u32x4{lo16(o[0], o[1]), lo16(o[2], o[3]), lo16(o[4], o[5]), lo16(o[6], o[7])});
+						st128(hv + kWht + 16,
+						      u32x4{lo16(o[8], o[9]), lo16(o[10], o[11]), lo16(o[12], o[13]), lo16(o[14], o[15])});
 					}
 					wave_lds_sync();
-					if (is_yl && h == 0) v[0] = (int)*(const int16_t*)(wv + kWht + yb * 2);
+					if (ln < 16 && !bpred) v[0] = (int)*(const int16_t*)(hv + kWht + 2 * ln);
 				}
-
-				// any AC coefficient in the MB? (raw, before dequant: conservative)
-				bool ac = false;
-				if (lane < 48) {
-#pragma unroll
-					for (int k = 0; k < 8; k++) ac |= (k > 0 || h == 1) && cf[k] != 0;
-				}
-				if (__ballot(ac) != 0ull) {
-					// inverse DCT, RFC 14.4 (vertical pass truncated to int16, then horizontal)
-					int o[8];
-#pragma unroll
-					for (int k = 0; k < 8; k++) o[k] = partner(v[k]);
-					int t[8];
+				// inverse DCT (RFC 14.4), whole 4x4 block per lane; DC-only shortcut when no lane
+				// of the wave has an AC coefficient ((dc+4)>>3 everywhere, exact)
+				if (__ballot(anyac && ln < 24 && act) != 0ull) {
+					int t4[16];
 #pragma unroll
 					for (int i = 0; i < 4; i++) {
-						const int r0 = h ? o[i] : v[i], r1 = h ? o[4 + i] : v[4 + i];
-						const int r2 = h ? v[i] : o[i], r3 = h ? v[4 + i] : o[4 + i];
-						const int a1 = r0 + r2, b1 = r0 - r2;
-						const int c1 = mul_s(r1) - mul_c(r3), d1 = mul_c(r1) + mul_s(r3);
-						t[i] = sx16(h ? b1 - c1 : a1 + d1);
-						t[4 + i] = sx16(h ? a1 - d1 : b1 + c1);
+						const int a1 = v[i] + v[8 + i], b1 = v[i] - v[8 + i];
+						const int c1 = mul_s(v[4 + i]) - mul_c(v[12 + i]), d1 = mul_c(v[4 + i]) + mul_s(v[12 + i]);
+						t4[i] = sx16(a1 + d1);
+						t4[12 + i] = sx16(a1 - d1);
+						t4[4 + i] = sx16(b1 + c1);
+						t4[8 + i] = sx16(b1 - c1);
 					}
 #pragma unroll
-					for (int rr = 0; rr < 2; rr++) {
-						const int* q = t + 4 * rr;
+					for (int i = 0; i < 4; i++) {
+						const int* q = t4 + 4 * i;
 						const int a1 = q[0] + q[2], b1 = q[0] - q[2];
 						const int c1 = mul_s(q[1]) - mul_c(q[3]), d1 = mul_c(q[1]) + mul_s(q[3]);
-						res[4 * rr + 0] = sx16((a1 + d1 + 4) >> 3);
-						res[4 * rr + 3] = sx16((a1 - d1 + 4) >> 3);
-						res[4 * rr + 1] = sx16((b1 + c1 + 4) >> 3);
-						res[4 * rr + 2] = sx16((b1 - c1 + 4) >> 3);
+						res[4 * i + 0] = sx16((a1 + d1 + 4) >> 3);
+						res[4 * i + 3] = sx16((a1 - d1 + 4) >> 3);
+						res[4 * i + 1] = sx16((b1 + c1 + 4) >> 3);
+						res[4 * i + 2] = sx16((b1 - c1 + 4) >> 3);
 					}
 				} else {
-					// DC-only blocks: the transform output is (dc + 4) >> 3 everywhere
-					const int pv0 = partner(v[0]);  // executed by every lane (DPP source must be live)
-					const int dc = h ? pv0 : v[0];
-					const int d = (dc + 4) >> 3;
+					const int d = (v[0] + 4) >> 3;
 #pragma unroll
-					for (int k = 0; k < 8; k++) res[k] = d;
+					for (int i = 0; i < 16; i++) res[i] = d;
+				}
+				if (ln < 24) {
+					uint8_t* rp = hv + kResid + ln * 32;
+					st128(rp, u32x4{lo16(res[0], res[1]), lo16(res[2], res[3]), lo16(res[4], res[5]), lo16(res[6], res[7])});
+					st128(rp + 16,
+					      u32x4{lo16(res[8], res[9]), lo16(res[10], res[11]), lo16(res[12], res[13]), lo16(res[14], res[15])});
 				}
 			}
-
 			STAMP(0);
-			// ------------------------------------------------ wait for MB(r-1, c+1)
-			if (r > 0 && !(VP8G_ABLATE & 8)) {
-				const uint32_t need = (r - 1) * C + ((c + 2 < C) ? c + 2 : C);
+
+			// ---------------------------------------------- wait: pair k-1's lower row 2 cols ahead
+			if (k > 0 && !(VP8G_ABLATE & 8)) {
+				const uint32_t need = (k - 1) * CP2 + ((t + 4 < CP2) ? t + 4 : CP2);
 				const uint32_t pw = (uint32_t)((wave + NW - 1) % NW);
 				uint32_t spins = 0;
 				uint64_t t0 = 0;
@@ -416,25 +545,36 @@ __global__ __launch_bounds__(NW * 64) void frame_kernel(const Vp8gFrameDesc* __r
 				}
 				asm volatile("" ::: "memory");
 			}
-
 			STAMP(1);
-			// ------------------------------------------------ borders + loop-filter top strip
-			if (!lf_only) {
+
+			// ---------------------------------------------- borders + loop-filter top strip
+			if (act) {
 				const bool top = r == 0;
-				if (lane < 4) {  // luma above row
-					st32(abY + 16 + 4 * lane, top ? 0x7F7F7F7Fu : ctx.rd(rec_off(c) + 4 * lane));
-				} else if (lane == 4) {  // luma above-right (row above the MB, cols x+16..x+19)
+				if (lf_only) {
+					// loop-filter-only mode: the MB's pixels come from the padded input image
+					const uint8_t* src = A.src;
+					if (ln < 16) {
+						const uint8_t* s = src + D.src_y + (size_t)(y0 + ln) * D.src_stride_y + x0;
+						st128(tY + (4 + ln) * 32 + slot * 16, u32x4{ld32(s), ld32(s + 4), ld32(s + 8), ld32(s + 12)});
+					} else {
+						const int p = (ln - 16) >> 3, row = ln & 7;
+						const uint8_t* s = src + (p ? D.src_v : D.src_u) + (size_t)(cy0 + row) * D.src_stride_uv + cx0;
+						st64((p ? tV : tU) + (4 + row) * 16 + slot * 8, u32x2{ld32(s), ld32(s + 4)});
+					}
+				} else if (ln < 4) {  // luma above row
+					st32(abY + 16 + 4 * ln, top ? 0x7F7F7F7Fu : ctx.rd(rec_off(cu) + 4 * ln));
+				} else if (ln == 4) {  // luma above-right (row above the MB, cols x+16..x+19)
 					uint32_t v4;
 					if (top) v4 = 0x7F7F7F7Fu;
-					else if (c + 1 < C) v4 = ctx.rd(rec_off(c + 1));
-					else v4 = (ctx.rd(rec_off(c) + 12) >> 24) * 0x01010101u;  // clamp to padded width
+					else if (cu + 1 < C) v4 = ctx.rd(rec_off(cu + 1));
+					else v4 = (ctx.rd(rec_off(cu) + 12) >> 24) * 0x01010101u;  // clamp to padded width
 					st32(abY + 32, v4);
-				} else if (lane < 9) {  // chroma above rows
-					const int k = lane - 5, p = k >> 1, dw = k & 1;
-					st32(abUV + 16 * p + 8 + 4 * dw, top ? 0x7F7F7F7Fu : ctx.rd(rec_off(c) + 16 + 8 * p + 4 * dw));
-				} else if (lane < 17) {  // left columns at the frame's left edge: 129
-					if (c == 0) st32(left + 4 * (lane - 9), 0x81818181u);
-				} else if (lane == 17) {  // corners at the left edge: 127 on the top row, else 129
+				} else if (ln < 9) {  // chroma above rows
+					const int q = ln - 5, p = q >> 1, dw = q & 1;
+					st32(abUV + 16 * p + 8 + 4 * dw, top ? 0x7F7F7F7Fu : ctx.rd(rec_off(cu) + 16 + 8 * p + 4 * dw));
+				} else if (ln < 17) {  // left columns at the frame's left edge: 129
+					if (c == 0) st32(left + 4 * (ln - 9), 0x81818181u);
+				} else if (ln == 17) {  // corners at the left edge: 127 on the top row, else 129
 					if (c == 0) {
 						const uint8_t pv = top ? 127 : 129;
 						abY[15] = pv;
@@ -442,106 +582,84 @@ __global__ __launch_bounds__(NW * 64) void frame_kernel(const Vp8gFrameDesc* __r
 						abUV[23] = pv;
 					}
 				}
-			}
-			if (lf_on && r > 0 && lane >= 32 && lane < 48) {  // filter state of the MB above
-				const int k = lane - 32;
-				if (k < 8) {
-					const int t = k >> 1, half = k & 1;
-					const uint32_t o = lf_off(c) + t * 16 + half * 8;
-					st64(tY + t * 32 + slot * 16 + half * 8, make_uint2(ctx.rd(o), ctx.rd(o + 4)));
-				} else {
-					const int p = (k - 8) >> 2, t = (k - 8) & 3;
-					const uint32_t o = lf_off(c) + 64 + p * 32 + t * 8;
-					st64((p ? tV : tU) + t * 16 + slot * 8, make_uint2(ctx.rd(o), ctx.rd(o + 4)));
+				if (lf_on && !top && ln >= 18 && ln < 30) {  // filter state of the MB above
+					if (ln < 22) {
+						st128(tY + (ln - 18) * 32 + slot * 16, ctx.rd128(lf_off(cu) + (ln - 18) * 16));
+					} else {
+						const int p = (ln - 22) >> 2, tr = (ln - 22) & 3;
+						st64((p ? tV : tU) + tr * 16 + slot * 8, ctx.rd64(lf_off(cu) + 64 + p * 32 + tr * 8));
+					}
 				}
 			}
 			wave_lds_sync();
-
 			STAMP(2);
-			// ------------------------------------------------ prediction + reconstruction
-			if (lf_only) {
-				// loop-filter-only mode: the MB's pixels come from the padded input image
-				const uint8_t* src = A.src;
-				if (lane < 32) {  // luma: 16 rows x 2 halves
-					const int row = lane >> 1, half = lane & 1;
-					const uint8_t* s = src + D.src_y + (size_t)(y0 + row) * D.src_stride_y + x0 + half * 8;
-					uint2 v2 = make_uint2(ld32(s), ld32(s + 4));
-					st64(tY + (4 + row) * 32 + slot * 16 + half * 8, v2);
-				} else if (lane < 48) {
-					const int k = lane - 32, p = k >> 3, row = k & 7;
-					const uint8_t* s = src + (p ? D.src_v : D.src_u) + (size_t)(cy0 + row) * D.src_stride_uv + cx0;
-					st64((p ? tV : tU) + (4 + row) * 16 + slot * 8, make_uint2(ld32(s), ld32(s + 4)));
-				}
-			} else {
+
+			// ---------------------------------------------- prediction + reconstruction
+			if (!lf_only) {
 				const bool have_above = r > 0, have_left = c > 0;
-				if (!bpred || is_uvl) {
-					// whole-block predictors (RFC 12.2; reference vp8_recon.c:152-212, 533-560, 605-651)
-					if (lane < 48) {
-						const bool yl = is_yl;
-						const int mode = yl ? (ymode > 4 ? 0 : ymode) : (uvmode > 3 ? 0 : uvmode);
-						const uint8_t* ab = yl ? abY + 16 : abUV + 16 * uvp + 8;
-						const uint8_t* lc = yl ? left : left + 16 + 8 * uvp;
-						const int blk = yl ? yb : uvb;
-						const int py = yl ? 4 * (blk >> 2) + 2 * h : 4 * (blk >> 1) + 2 * h;
-						const int pxo = yl ? 4 * (blk & 3) : 4 * (blk & 1);
-						int dcv = 128;
-						if (mode == 0) {
-							uint32_t sa = 0, sl = 0;
-							if (yl) {
-								sa = bsum4(ld32(ab)) + bsum4(ld32(ab + 4)) + bsum4(ld32(ab + 8)) + bsum4(ld32(ab + 12));
-								sl = bsum4(ld32(lc)) + bsum4(ld32(lc + 4)) + bsum4(ld32(lc + 8)) + bsum4(ld32(lc + 12));
-							} else {
-								sa = bsum4(ld32(ab)) + bsum4(ld32(ab + 4));
-								sl = bsum4(ld32(lc)) + bsum4(ld32(lc + 4));
-							}
-							const int sh = yl ? 4 : 3;
-							if (have_above && have_left) dcv = (int)(sa + sl + (1u << sh)) >> (sh + 1);
-							else if (have_left) dcv = (int)(sl + (1u << (sh - 1))) >> sh;
-							else if (have_above) dcv = (int)(sa + (1u << (sh - 1))) >> sh;
+				if (act && ln < 24 && (ln >= 16 || !bpred)) {
+					// whole-block predictors (RFC 12.2; reference vp8_recon.c:152-212, 533-560, 605-651),
+					// one 4x4 block per lane
+					const bool yl = ln < 16;
+					const int p = (ln - 16) >> 2;  // chroma plane (chroma lanes)
+					const int blk = yl ? ln : (ln & 3);
+					const int bx = yl ? (blk & 3) : (blk & 1), by = yl ? (blk >> 2) : (blk >> 1);
+					const uint8_t* ab = yl ? abY + 16 : abUV + 16 * p + 8;
+					const uint8_t* lc = yl ? left : left + 16 + 8 * p;
+					const int mode = yl ? (ymode > 4 ? 0 : ymode) : (uvmode > 3 ? 0 : uvmode);
+					int dcv = 128;
+					{
+						uint32_t sa = bsum4(ld32(ab)) + bsum4(ld32(ab + 4));
+						uint32_t sl = bsum4(ld32(lc)) + bsum4(ld32(lc + 4));
+						if (yl) {
+							sa += bsum4(ld32(ab + 8)) + bsum4(ld32(ab + 12));
+							sl += bsum4(ld32(lc + 8)) + bsum4(ld32(lc + 12));
 						}
-						const uint32_t aw = ld32(ab + pxo);
-						const int P = (int)u8(ab - 1);
-						uint8_t* dst = yl ? tY + (4 + py) * 32 + slot * 16 + pxo
-						                  : (uvp ? tV : tU) + (4 + py) * 16 + slot * 8 + pxo;
-						const int dstride = yl ? 32 : 16;
+						const int sh = yl ? 4 : 3;
+						if (have_above && have_left) dcv = (int)(sa + sl + (1u << sh)) >> (sh + 1);
+						else if (have_left) dcv = (int)(sl + (1u << (sh - 1))) >> sh;
+						else if (have_above) dcv = (int)(sa + (1u << (sh - 1))) >> sh;
+					}
+					const uint32_t aw = ld32(ab + 4 * bx);
+					const uint32_t lw = ld32(lc + 4 * by);
+					const int P = (int)ab[-1];
+					uint8_t* dst = yl ? tY + (4 + 4 * by) * 32 + slot * 16 + 4 * bx
+					                  : (p ? tV : tU) + (4 + 4 * by) * 16 + slot * 8 + 4 * bx;
+					const int dstride = yl ? 32 : 16;
+					const u32x4 r01 = ld128(hv + kResid + ln * 32), r23 = ld128(hv + kResid + ln * 32 + 16);
+					const uint32_t rw[8] = {r01.x, r01.y, r01.z, r01.w, r23.x, r23.y, r23.z, r23.w};
 #pragma unroll
-						for (int rr = 0; rr < 2; rr++) {
-							const int L = (int)u8(lc + py + rr);
-							int px4[4];
+					for (int rr = 0; rr < 4; rr++) {
+						const int L = ubyte(lw, rr);
+						int px4[4];
 #pragma unroll
-							for (int k = 0; k < 4; k++) {
-								const int a = ubyte(aw, k);
-								const int pred = mode == 1 ? a : (mode == 2 ? L : (mode == 3 ? sat8(L + a - P) : dcv));
-								px4[k] = sat8(pred + res[4 * rr + k]);
-							}
-							st32(dst + rr * dstride, pack4(px4[0], px4[1], px4[2], px4[3]));
+						for (int cc = 0; cc < 4; cc++) {
+							const int a = ubyte(aw, cc);
+							const int pred = mode == 1 ? a : (mode == 2 ? L : (mode == 3 ? sat8(L + a - P) : dcv));
+							const int rv = (int)(int16_t)((rw[(4 * rr + cc) >> 1] >> (16 * (cc & 1))) & 0xFFFFu);
+							px4[cc] = sat8(pred + rv);
 						}
+						st32(dst + rr * dstride, pack4(px4[0], px4[1], px4[2], px4[3]));
 					}
 				}
-				if (bpred && !(VP8G_ABLATE & 2)) {
+				wave_lds_sync();
+				const bool bp_lane = act && bpred;
+				if (__ballot(bp_lane) != 0ull && !(VP8G_ABLATE & 2)) {
 					// B_PRED: 16 sub-blocks along the 2i+j wavefront (10 steps, <= 2 sub-blocks
 					// each), using already reconstructed pixels (reference vp8_recon.c:454-530)
-					int16_t* rs = (int16_t*)(wv + kResid);
-					if (is_yl) {
-						uint4 pk;
-						pk.x = (uint32_t)(res[0] & 0xFFFF) | ((uint32_t)res[1] << 16);
-						pk.y = (uint32_t)(res[2] & 0xFFFF) | ((uint32_t)res[3] << 16);
-						pk.z = (uint32_t)(res[4] & 0xFFFF) | ((uint32_t)res[5] << 16);
-						pk.w = (uint32_t)(res[6] & 0xFFFF) | ((uint32_t)res[7] << 16);
-						*(uint4*)(wv + kResid + lane * 16) = pk;
-					}
-					const uint4 bm = *(const uint4*)(A.bmode + m * 16);
-					const uint32_t bmw[4] = {(uint32_t)__builtin_amdgcn_readfirstlane((int)bm.x),
-					                         (uint32_t)__builtin_amdgcn_readfirstlane((int)bm.y),
-					                         (uint32_t)__builtin_amdgcn_readfirstlane((int)bm.z),
-					                         (uint32_t)__builtin_amdgcn_readfirstlane((int)bm.w)};
-					wave_lds_sync();
-					const int g = (lane >> 4) & 1, p = lane & 15;
-					uint8_t* edge = wv + kEdge + g * 16;
+					const u32x4 bm0 = u32x4{(uint32_t)rdlane((int)cur.a.x, 25), (uint32_t)rdlane((int)cur.a.y, 25),
+					                        (uint32_t)rdlane((int)cur.a.z, 25), (uint32_t)rdlane((int)cur.a.w, 25)};
+					const u32x4 bm1 = u32x4{(uint32_t)rdlane((int)cur.a.x, 57), (uint32_t)rdlane((int)cur.a.y, 57),
+					                        (uint32_t)rdlane((int)cur.a.z, 57), (uint32_t)rdlane((int)cur.a.w, 57)};
+					const u32x4 bmw = hh ? bm1 : bm0;
+					const int g = (ln >> 4) & 1, p = ln & 15;
+					uint8_t* edge = hv + kEdge + g * 16;
+					const int16_t* rs = (const int16_t*)(hv + kResid);
+					const uint16_t* bptab = (const uint16_t*)(smem + kBpTable);
 					for (int s = 0; s < 10; s++) {
 						const int ilo = s <= 3 ? 0 : (s - 2) >> 1;
 						const int i = ilo + g, j = s - 2 * i;
-						const bool valid = lane < 32 && i <= 3 && j >= 0 && j <= 3;
+						const bool valid = bp_lane && i <= 3 && j >= 0 && j <= 3;
 						// (1) gather the 13 edge pixels of each sub-block of this step
 						if (valid && p <= 12) {
 							const int e = p;
@@ -553,223 +671,137 @@ __global__ __launch_bounds__(NW * 64) void frame_kernel(const Vp8gFrameDesc* __r
 								srcp = (i == 0) ? abY + 16 + 4 * j - 1
 								                : ((j == 0) ? left + 4 * i - 1 : tY + (3 + 4 * i) * 32 + slot * 16 + 4 * j - 1);
 							} else {
-								const int k = e - 5;
-								if (j == 3 && k >= 4) srcp = abY + 32 + (k - 4);
-								else srcp = (i == 0) ? abY + 16 + 4 * j + k : tY + (3 + 4 * i) * 32 + slot * 16 + 4 * j + k;
+								const int kk = e - 5;
+								if (j == 3 && kk >= 4) srcp = abY + 32 + (kk - 4);
+								else srcp = (i == 0) ? abY + 16 + 4 * j + kk : tY + (3 + 4 * i) * 32 + slot * 16 + 4 * j + kk;
 							}
 							edge[e < 4 ? e : (e == 4 ? 7 : e + 3)] = *srcp;
 						}
 						wave_lds_sync();
-						// (2) predict + add residual, one pixel per lane
+						// (2) predict + add residual, one pixel per lane (branch-free)
 						if (valid) {
-							const uint4 E = *(const uint4*)edge;
+							const u32x4 E = ld128(edge);
 							const int b = 4 * i + j;
-							const int mode = (int)((bmw[b >> 2] >> (8 * (b & 3))) & 0xFFu);
+							const int mode = byte16(bmw, b);
 							const int rr = p >> 2, cc = p & 3;
-							int pred;
-							if (mode == 0) {
-								pred = (int)(bsum4(E.x) + bsum4(E.z) + 4) >> 3;
-							} else if (mode == 1) {
-								pred = sat8(ubyte(E.x, 3 - rr) + ubyte(E.z, cc) - ubyte(E.y, 3));
-							} else if (mode <= 9) {
-								const uint32_t t = bptab[mode * 16 + p];
-								const int xa = byte16(E.x, E.y, E.z, E.w, (int)(t & 15));
-								const int xb = byte16(E.x, E.y, E.z, E.w, (int)((t >> 4) & 15));
-								const int xc = byte16(E.x, E.y, E.z, E.w, (int)((t >> 8) & 15));
-								const uint32_t kind = t >> 12;
-								pred = kind == 0 ? (xa + 2 * xb + xc + 2) >> 2 : (kind == 1 ? (xa + xb + 1) >> 1 : xa);
-							} else {
-								pred = 128;
-							}
-							const int rv = rs[b * 16 + p];
-							tY[(4 + 4 * i + rr) * 32 + slot * 16 + 4 * j + cc] = (uint8_t)sat8(pred + rv);
+							const uint32_t tb = bptab[(mode & 15) * 16 + p];
+							const int xa = byte16(E, (int)(tb & 15));
+							const int xb = byte16(E, (int)((tb >> 4) & 15));
+							const int xc = byte16(E, (int)((tb >> 8) & 15));
+							const uint32_t kind = tb >> 12;
+							const int vt = kind == 0 ? (xa + 2 * xb + xc + 2) >> 2 : (kind == 1 ? (xa + xb + 1) >> 1 : xa);
+							const int vdc = (int)(bsum4(E.x) + bsum4(E.z) + 4) >> 3;
+							const int vtm = sat8(ubyte(E.x, 3 - rr) + ubyte(E.z, cc) - ubyte(E.y, 3));
+							const int pred = mode == 0 ? vdc : (mode == 1 ? vtm : (mode <= 9 ? vt : 128));
+							tY[(4 + 4 * i + rr) * 32 + slot * 16 + 4 * j + cc] = (uint8_t)sat8(pred + rs[b * 16 + p]);
 						}
 						wave_lds_sync();
 					}
 				}
 			}
 			wave_lds_sync();
-
 			STAMP(3);
-			// ------------------------------------------------ save unfiltered context
-			if (!lf_only) {
-				if (lane < 4) {  // bottom rows -> ctx_rec[c] for the next MB row
-					if (r + 1 < R) {
-						const uint8_t* t = lane < 2 ? tY + 19 * 32 + slot * 16 + 8 * lane
-						                            : (lane == 2 ? tU : tV) + 11 * 16 + slot * 8;
-						const uint32_t o = rec_off(c) + 8 * lane;  // Y 0..15, U 16..23, V 24..31
-						ctx.wr(o, ld32(t));
-						ctx.wr(o + 4, ld32(t + 4));
-					}
-				} else if (lane == 4) {  // corner for the next MB
+
+			// ---------------------------------------------- save unfiltered context
+			if (act && !lf_only) {
+				// right column -> left column of the next MB (Y 16, U 8, V 8 lanes)
+				const uint8_t* sp = ln < 16 ? tY + (4 + ln) * 32 + slot * 16 + 15
+				                            : (ln < 24 ? tU : tV) + (4 + (ln & 7)) * 16 + slot * 8 + 7;
+				const uint8_t pxv = *sp;
+				if (ln == 0) ctx.wr128(rec_off(cu), ld128(tY + 19 * 32 + slot * 16));  // bottom rows -> ctx_rec[c]
+				else if (ln == 1) ctx.wr64(rec_off(cu) + 16, ld64(tU + 11 * 16 + slot * 8));
+				else if (ln == 2) ctx.wr64(rec_off(cu) + 24, ld64(tV + 11 * 16 + slot * 8));
+				else if (ln == 3) {  // corner for the next MB
 					abY[15] = abY[31];
 					abUV[7] = abUV[15];
 					abUV[23] = abUV[31];
-				} else if (lane >= 32) {  // right column -> left column of the next MB
-					const int k = lane - 32;
-					if (k < 16) left[k] = tY[(4 + k) * 32 + slot * 16 + 15];
-					else if (k < 24) left[k] = tU[(4 + k - 16) * 16 + slot * 8 + 7];
-					else left[k] = tV[(4 + k - 24) * 16 + slot * 8 + 7];
 				}
+				left[ln] = pxv;
 			}
 			wave_lds_sync();
-
 			STAMP(4);
-			// ------------------------------------------------ loop filter MB(r, c)
+
+			// ---------------------------------------------- loop filter MB(r, c)
 			if (lf_on && !(VP8G_ABLATE & 1)) {
-				const uint8_t* lp = D.lf[seg][bpred ? 1 : 0];
-				const int E = lp[0], I = lp[1], T = lp[2];
-				if (E != 0) {
+				const uint8_t* lp = smem + kLfTable + seg * 8 + (bpred ? 4 : 0);
+				const int E = lp[0], I = lp[1], Tt = lp[2];
+				const bool en = act && E != 0;
+				if (__ballot(en) != 0ull) {
 					const bool inner = hasc != 0 || bpred;
-					// vertical edges: one line per lane along a pixel row (Y 16, U 8, V 8)
-					if (lane < 32) {
-						const bool isy = lane < 16;
-						int px[20];
-						if (isy) {
-							uint8_t* rowp = tY + (4 + lane) * 32;
-#pragma unroll
-							for (int k = 0; k < 5; k++) {
-								const uint32_t w4 = ld32(rowp + 4 * ((slot * 4 - 1 + k) & 7));
-#pragma unroll
-								for (int b = 0; b < 4; b++) px[4 * k + b] = ubyte(w4, b);
-							}
-						} else {
-							const int k2 = lane - 16, p = k2 >> 3, row = k2 & 7;
-							uint8_t* rowp = (p ? tV : tU) + (4 + row) * 16;
-#pragma unroll
-							for (int k = 0; k < 3; k++) {
-								const uint32_t w4 = ld32(rowp + 4 * ((slot * 2 - 1 + k) & 3));
-#pragma unroll
-								for (int b = 0; b < 4; b++) px[4 * k + b] = ubyte(w4, b);
-							}
-#pragma unroll
-							for (int k = 12; k < 20; k++) px[k] = 0;
-						}
-						lf_line(px, simple, c > 0, inner, isy, E, I, T);
-						if (isy) {
-							uint8_t* rowp = tY + (4 + lane) * 32;
-#pragma unroll
-							for (int k = 0; k < 5; k++)
-								st32(rowp + 4 * ((slot * 4 - 1 + k) & 7), pack4(px[4 * k], px[4 * k + 1], px[4 * k + 2], px[4 * k + 3]));
-						} else if (!simple) {
-							const int k2 = lane - 16, p = k2 >> 3, row = k2 & 7;
-							uint8_t* rowp = (p ? tV : tU) + (4 + row) * 16;
-#pragma unroll
-							for (int k = 0; k < 3; k++)
-								st32(rowp + 4 * ((slot * 2 - 1 + k) & 3), pack4(px[4 * k], px[4 * k + 1], px[4 * k + 2], px[4 * k + 3]));
-						}
-					}
-					wave_lds_sync();
-					// horizontal edges: one line per lane down a pixel column
-					if (lane < 32) {
-						const bool isy = lane < 16;
-						int px[20];
-						uint8_t* colp;
-						int stride;
-						if (isy) {
-							colp = tY + slot * 16 + lane;
-							stride = 32;
-						} else {
-							const int k2 = lane - 16, p = k2 >> 3;
-							colp = (p ? tV : tU) + slot * 8 + (k2 & 7);
-							stride = 16;
-						}
-						const int n = isy ? 20 : 12;
-#pragma unroll
-						for (int k = 0; k < 20; k++) px[k] = k < n ? (int)colp[k * stride] : 0;
-						lf_line(px, simple, r > 0, inner, isy, E, I, T);
-						if (isy || !simple) {
-#pragma unroll
-							for (int k = 1; k < 19; k++)
-								if (k < n) colp[k * stride] = (uint8_t)px[k];
-						}
-					}
-					wave_lds_sync();
+					if (simple) lf_mb<true>(tY, tU, tV, ln, slot, en, c > 0, r > 0, inner, E, I, Tt);
+					else lf_mb<false>(tY, tU, tV, ln, slot, en, c > 0, r > 0, inner, E, I, Tt);
 				}
 			}
-
 			STAMP(5);
-			// ------------------------------------------------ store final pixels
-			// 8-byte chunk store with crop; falls back to bytes at the right edge / misalignment
-			auto put8 = [&](uint8_t* plane, uint32_t stride, uint32_t vis_w, uint32_t vis_h, uint32_t row, uint32_t col,
-			                uint2 v) {
+
+			// ---------------------------------------------- store final pixels
+			// crop-aware store of an 8- or 16-byte row piece from LDS
+			auto put = [&](uint8_t* plane, uint32_t stride, uint32_t vis_w, uint32_t vis_h, uint32_t row, uint32_t col,
+			               const uint8_t* src, bool w16) {
 				if (row >= vis_h || col >= vis_w || (VP8G_ABLATE & 4)) return;
 				uint8_t* d = plane + (size_t)row * stride + col;
-				const uint32_t n = vis_w - col;
-				if (n >= 8 && (((uintptr_t)d) & 7) == 0) {
-					*(uint2*)d = v;
+				const uint32_t n = vis_w - col, wdt = w16 ? 16u : 8u;
+				if (n >= wdt && (((uintptr_t)d) & (wdt - 1)) == 0) {
+					if (w16) *(u32x4*)d = ld128(src);
+					else *(u32x2*)d = ld64(src);
 				} else {
-					const uint32_t cnt = n < 8 ? n : 8;
-					for (uint32_t k = 0; k < cnt; k++) d[k] = (uint8_t)(((k < 4 ? v.x : v.y) >> (8 * (k & 3))) & 0xFF);
+					const uint32_t cnt = n < wdt ? n : wdt;
+					for (uint32_t q = 0; q < cnt; q++) d[q] = src[q];
 				}
 			};
 			if (!lf_on) {
 				// unfiltered: MB(r, c) is final as soon as it is reconstructed
-				if (lane < 32) {
-					const int row = lane >> 1, half = lane & 1;
-					put8(outY, sy, W, H, y0 + row, x0 + half * 8, ld64(tY + (4 + row) * 32 + slot * 16 + half * 8));
-				} else if (lane < 48) {
-					const int k = lane - 32, p = k >> 3, row = k & 7;
-					put8(p ? outV : outU, suv, CW, CH, cy0 + row, cx0, ld64((p ? tV : tU) + (4 + row) * 16 + slot * 8));
+				if (act) {
+					if (ln < 16) put(outY, sy, W, H, y0 + ln, x0, tY + (4 + ln) * 32 + slot * 16, true);
+					else {
+						const int p = (ln - 16) >> 3, row = ln & 7;
+						put(p ? outV : outU, suv, CW, CH, cy0 + row, cx0, (p ? tV : tU) + (4 + row) * 16 + slot * 8, false);
+					}
 				}
 			} else {
 				const bool last_row = r + 1 == R;
-				// flush one finished MB column `cc` held in ring slot `sl` (rows 0..11 luma, 0..3
-				// chroma final; the bottom 4 rows go to ctx_lf for the row below, or out if last row)
-				auto flush_col = [&](uint32_t ccol, int sl) {
-					const uint32_t xx = ccol * 16, cxx = ccol * 8;
-					if (lane >= 8 && lane < 32) {
-						const int k = lane - 8, row = k >> 1, half = k & 1;
-						put8(outY, sy, W, H, y0 + row, xx + half * 8, ld64(tY + (4 + row) * 32 + sl * 16 + half * 8));
-					} else if (lane >= 32 && lane < 40) {
-						const int k = lane - 32, t = k >> 1, half = k & 1;
-						const uint2 v2 = ld64(tY + (16 + t) * 32 + sl * 16 + half * 8);
-						if (last_row) put8(outY, sy, W, H, y0 + 12 + t, xx + half * 8, v2);
-						else {
-							const uint32_t o = lf_off(ccol) + t * 16 + half * 8;
-							ctx.wr(o, v2.x);
-							ctx.wr(o + 4, v2.y);
+				const bool last_col = cu + 1 == C;
+				const uint16_t* ftab = (const uint16_t*)(smem + kFlushTable);
+				const int rounds = __ballot(act && last_col) != 0ull ? 3 : 2;
+				for (int rd = 0; rd < rounds; rd++) {
+					const uint32_t e = ftab[rd * 32 + ln];
+					const int pl = (e >> 8) & 3, kind = (e >> 6) & 3, prev = (e >> 5) & 1, kk = e & 15;
+					const bool ok = act && (e & 0x8000u) && (kind != 0 || r > 0) && (prev ? c > 0 : (kind == 0 || last_col));
+					if (ok) {
+						const uint32_t col = prev ? cu - 1 : cu;
+						const int sl = prev ? slot ^ 1 : slot;
+						if (pl == 0) {
+							const int trow = kind == 0 ? kk : (kind == 1 ? 4 + kk : 16 + kk);
+							const uint8_t* src = tY + trow * 32 + sl * 16;
+							if (kind == 2 && !last_row) ctx.wr128(lf_off(col) + kk * 16, ld128(src));
+							else put(outY, sy, W, H, kind == 0 ? y0 - 4 + kk : y0 + trow - 4, col * 16, src, true);
+						} else {
+							const int trow = kind == 0 ? kk : (kind == 1 ? 4 + kk : 8 + kk);
+							const uint8_t* src = (pl == 2 ? tV : tU) + trow * 16 + sl * 8;
+							if (kind == 2 && !last_row) ctx.wr64(lf_off(col) + 64 + (pl - 1) * 32 + kk * 8, ld64(src));
+							else put(pl == 2 ? outV : outU, suv, CW, CH, kind == 0 ? cy0 - 4 + kk : cy0 + trow - 4, col * 8, src, false);
 						}
-					} else if (lane >= 48 && lane < 56) {
-						const int k = lane - 48, p = k >> 2, t = k & 3;
-						put8(p ? outV : outU, suv, CW, CH, cy0 + t, cxx, ld64((p ? tV : tU) + (4 + t) * 16 + sl * 8));
-					} else if (lane >= 56) {
-						const int k = lane - 56, p = k >> 2, t = k & 3;
-						const uint2 v2 = ld64((p ? tV : tU) + (8 + t) * 16 + sl * 8);
-						if (last_row) put8(p ? outV : outU, suv, CW, CH, cy0 + 4 + t, cxx, v2);
-						else {
-							const uint32_t o = lf_off(ccol) + 64 + p * 32 + t * 8;
-							ctx.wr(o, v2.x);
-							ctx.wr(o + 4, v2.y);
-						}
-					}
-				};
-				// rows 12..15 of the MB above are final now (LF(r,c) was their last writer)
-				if (r > 0) {
-					if (lane < 8) {
-						const int t = lane >> 1, half = lane & 1;
-						put8(outY, sy, W, H, y0 - 4 + t, x0 + half * 8, ld64(tY + t * 32 + slot * 16 + half * 8));
-					} else if (lane >= 40 && lane < 48) {
-						const int k = lane - 40, p = k >> 2, t = k & 3;
-						put8(p ? outV : outU, suv, CW, CH, cy0 - 4 + t, cx0, ld64((p ? tV : tU) + t * 16 + slot * 8));
 					}
 				}
-				if (c > 0) flush_col(c - 1, slot ^ 1);
-				if (c + 1 == C) flush_col(c, slot);
 			}
 			wave_lds_sync();
-
 			STAMP(6);
-			// ------------------------------------------------ publish progress
+
+			// ---------------------------------------------- publish progress
 			ctx.publish_fence();
 			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-			if (lane == 0) __hip_atomic_store(prog + wave, r * C + c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+			if (lane == 0) __hip_atomic_store(prog + wave, k * CP2 + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 			STAMP(7);
 		}
 	}
 #ifdef VP8G_STAMPS
 	if (lane0 == 0)
 		for (int i = 0; i < 8; i++) atomicAdd(&g_vp8g_stamps[i], (unsigned long long)st_acc[i]);
+	if (f == 0 && lane0 == 0 && wave < 32) g_vp8g_wave_times[2 * wave + 1] = __builtin_amdgcn_s_memrealtime();
+	if (f == 0 && lane0 == 0 && wave == 0) {
+		g_vp8g_stamps[8] = __builtin_amdgcn_s_memtime();
+		g_vp8g_stamps[9] = __builtin_amdgcn_s_memrealtime();
+	}
 #endif
 }
 
@@ -789,6 +821,9 @@ hipError_t launch_t(const Vp8gFrameDesc* d_descs, uint32_t n, const Vp8gBatchArr
 }  // namespace
 
 #ifdef VP8G_STAMPS
+extern "C" __attribute__((visibility("default"))) int vp8g_debug_wave_times(unsigned long long* out) {
+	return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vp8g_wave_times), sizeof(unsigned long long) * 64) == hipSuccess ? 0 : -1;
+}
 extern "C" __attribute__((visibility("default"))) int vp8g_debug_stamps(unsigned long long* out, int reset) {
 	if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vp8g_stamps), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
 	if (reset) {
@@ -799,20 +834,26 @@ extern "C" __attribute__((visibility("default"))) int vp8g_debug_stamps(unsigned
 }
 #endif
 
+uint32_t pick_waves(uint32_t waves_hint, uint32_t max_mb_rows) {
+	static const uint32_t kSupported[] = {1, 2, 4, 8, 12, 16};
+	uint32_t want = waves_hint ? waves_hint : 8;
+	const uint32_t pairs = (max_mb_rows + 1) / 2;
+	if (want > pairs) want = pairs;  // no point in more waves than MB row pairs
+	uint32_t nw = 1;
+	for (uint32_t s : kSupported)
+		if (s <= want) nw = s;
+	return nw;
+}
+
 hipError_t launch_frames(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const Vp8gBatchArrays& arrays,
                          uint8_t* d_out, uint32_t ctx_cols, uint32_t max_mb_rows, uint8_t* global_ctx,
                          hipStream_t stream, uint32_t waves_hint) {
 	if (n_frames == 0) return hipSuccess;
-	static const uint32_t kSupported[] = {1, 2, 4, 8, 12, 16};
-	uint32_t want = waves_hint ? waves_hint : 16;
-	if (want > max_mb_rows) want = max_mb_rows;  // no point in more waves than MB rows
-	uint32_t nw = 1;
-	for (uint32_t s : kSupported)
-		if (s <= want) nw = s;
+	const uint32_t nw = pick_waves(waves_hint, max_mb_rows);
 	const bool g = global_ctx != nullptr;
-#define VP8G_CASE(N)                                                                                         \
-	case N:                                                                                                  \
-		return g ? launch_t<N, true>(d_descs, n_frames, arrays, d_out, ctx_cols, global_ctx, stream)        \
+#define VP8G_CASE(N)                                                                                  \
+	case N:                                                                                           \
+		return g ? launch_t<N, true>(d_descs, n_frames, arrays, d_out, ctx_cols, global_ctx, stream) \
 		         : launch_t<N, false>(d_descs, n_frames, arrays, d_out, ctx_cols, nullptr, stream);
 	switch (nw) {
 		VP8G_CASE(1)
