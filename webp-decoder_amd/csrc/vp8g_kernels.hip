@@ -653,47 +653,40 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					                        (uint32_t)rdlane((int)cur.a.z, 57), (uint32_t)rdlane((int)cur.a.w, 57)};
 					const u32x4 bmw = hh ? bm1 : bm0;
 					const int g = (ln >> 4) & 1, p = ln & 15;
-					uint8_t* edge = hv + kEdge + g * 16;
 					const int16_t* rs = (const int16_t*)(hv + kResid);
 					const uint16_t* bptab = (const uint16_t*)(smem + kBpTable);
 					for (int s = 0; s < 10; s++) {
 						const int ilo = s <= 3 ? 0 : (s - 2) >> 1;
 						const int i = ilo + g, j = s - 2 * i;
-						const bool valid = bp_lane && i <= 3 && j >= 0 && j <= 3;
-						// (1) gather the 13 edge pixels of each sub-block of this step
-						if (valid && p <= 12) {
-							const int e = p;
-							const uint8_t* srcp;
-							if (e < 4) {
-								const int yl = 4 * i + 3 - e;
-								srcp = (j == 0) ? left + yl : tY + (4 + yl) * 32 + slot * 16 + 4 * j - 1;
-							} else if (e == 4) {
-								srcp = (i == 0) ? abY + 16 + 4 * j - 1
-								                : ((j == 0) ? left + 4 * i - 1 : tY + (3 + 4 * i) * 32 + slot * 16 + 4 * j - 1);
-							} else {
-								const int kk = e - 5;
-								if (j == 3 && kk >= 4) srcp = abY + 32 + (kk - 4);
-								else srcp = (i == 0) ? abY + 16 + 4 * j + kk : tY + (3 + 4 * i) * 32 + slot * 16 + 4 * j + kk;
-							}
-							edge[e < 4 ? e : (e == 4 ? 7 : e + 3)] = *srcp;
-						}
-						wave_lds_sync();
-						// (2) predict + add residual, one pixel per lane (branch-free)
-						if (valid) {
-							const u32x4 E = ld128(edge);
+						if (bp_lane && i <= 3 && j >= 0 && j <= 3) {
+							// Each pixel lane assembles the sub-block's 13 edge pixels itself (one LDS round
+							// trip): edge rules of reference vp8_recon.c:464-504 -- the row above is the MB's
+							// above row when i == 0, the left column the MB's left column when j == 0, and
+							// the above-right of the last sub-block column always comes from the MB above.
 							const int b = 4 * i + j;
 							const int mode = byte16(bmw, b);
 							const int rr = p >> 2, cc = p & 3;
+							const uint8_t* arow = (i == 0) ? abY + 16 : tY + (3 + 4 * i) * 32 + slot * 16;
+							const uint32_t a03 = ld32(arow + 4 * j);
+							const uint32_t a47 = ld32(j == 3 ? abY + 32 : arow + 4 * j + 4);
+							const uint8_t* lcol = (j == 0) ? left + 4 * i : tY + (4 + 4 * i) * 32 + slot * 16 + 4 * j - 1;
+							const int ls = (j == 0) ? 1 : 32;
+							const uint32_t l0 = lcol[0], l1 = lcol[ls], l2 = lcol[2 * ls], l3 = lcol[3 * ls];
+							const uint8_t* pp = (i == 0) ? abY + 15 + 4 * j
+							                             : ((j == 0) ? left + 4 * i - 1 : tY + (3 + 4 * i) * 32 + slot * 16 + 4 * j - 1);
+							const uint32_t pv = *pp;
 							const uint32_t tb = bptab[(mode & 15) * 16 + p];
+							const int rv = rs[b * 16 + p];
+							const u32x4 E = u32x4{l3 | (l2 << 8) | (l1 << 16) | (l0 << 24), pv << 24, a03, a47};
 							const int xa = byte16(E, (int)(tb & 15));
 							const int xb = byte16(E, (int)((tb >> 4) & 15));
 							const int xc = byte16(E, (int)((tb >> 8) & 15));
 							const uint32_t kind = tb >> 12;
 							const int vt = kind == 0 ? (xa + 2 * xb + xc + 2) >> 2 : (kind == 1 ? (xa + xb + 1) >> 1 : xa);
 							const int vdc = (int)(bsum4(E.x) + bsum4(E.z) + 4) >> 3;
-							const int vtm = sat8(ubyte(E.x, 3 - rr) + ubyte(E.z, cc) - ubyte(E.y, 3));
+							const int vtm = sat8((int)ubyte(E.x, 3 - rr) + (int)ubyte(a03, cc) - (int)pv);
 							const int pred = mode == 0 ? vdc : (mode == 1 ? vtm : (mode <= 9 ? vt : 128));
-							tY[(4 + 4 * i + rr) * 32 + slot * 16 + 4 * j + cc] = (uint8_t)sat8(pred + rs[b * 16 + p]);
+							tY[(4 + 4 * i + rr) * 32 + slot * 16 + 4 * j + cc] = (uint8_t)sat8(pred + rv);
 						}
 						wave_lds_sync();
 					}
