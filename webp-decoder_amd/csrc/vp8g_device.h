@@ -15,20 +15,22 @@ constexpr int kLfU = 640;     // chroma tiles: 12 rows x 16 cols (4 above + 8 MB
 constexpr int kLfV = 832;
 constexpr int kAbY = 1024;    // luma above row: [15] corner P, [16..31] A, [32..35] above-right
 constexpr int kAbUV = 1072;   // chroma above rows: U P@7 A@8..15, V P@23 A@24..31
-constexpr int kLeft = 1104;   // unfiltered left columns: Y 0..15, U 16..23, V 24..31
-constexpr int kResid = 1136;  // residual of the MB: 25 blocks (16 Y, 4 U, 4 V, Y2 slot) x 16 int16
-constexpr int kEdge = 1936;   // B_PRED edge arrays of the (at most 2) sub-blocks of a step
-constexpr int kWht = 1968;    // 16 int16 luma DCs out of the inverse WHT
-constexpr int kHalfBytes = 2000;
+constexpr int kColY = 1104;   // B_PRED: luma columns 11, 7, 3 of the MB (16 B each, in that order),
+                              // so that the left column of sub-block column j is at kLeft - 16 j
+constexpr int kLeft = 1152;   // unfiltered left columns: Y 0..15, U 16..23, V 24..31
+constexpr int kResid = 1184;  // residual of the MB: 25 blocks (16 Y, 4 U, 4 V, Y2 slot) x 16 int16
+constexpr int kWht = 1984;    // 16 int16 luma DCs out of the inverse WHT
+constexpr int kHalfBytes = 2016;
 constexpr int kWaveBytes = 2 * kHalfBytes;
 
 // Workgroup header.
-constexpr int kProgress = 0;    // 16 x u32 progress words (one per wave)
-constexpr int kBpTable = 64;    // B_PRED predictor table: 16 modes x 16 px x u16
-constexpr int kDqTable = 576;   // 4 segments x 6 int16 dequant factors of this frame
-constexpr int kLfTable = 624;   // 4 segments x 2 (B_PRED?) x {E, I, T, 0}
-constexpr int kFlushTable = 656;  // 3 rounds x 32 lanes x u16 store tasks
-constexpr int kHdrBytes = 848;
+constexpr int kProgress = 0;      // 16 x u32 progress words (one per wave)
+constexpr int kBpTable = 64;      // B_PRED predictor table: 11 modes x 16 px x {perm selectors, byte mask}
+constexpr int kBpModes = 11;      // modes 0..9 + one constant-128 entry for out-of-range modes
+constexpr int kDqTable = kBpTable + kBpModes * 16 * 8;  // 4 segments x 6 int16 dequant factors
+constexpr int kLfTable = kDqTable + 48;                 // 4 segments x 2 (B_PRED?) x {E, I, T, 0}
+constexpr int kFlushTable = kLfTable + 32;              // 3 rounds x 32 lanes x u16 store tasks
+constexpr int kHdrBytes = kFlushTable + 192;
 
 // Shared per-MB-column context (one frame per workgroup).
 constexpr int kCtxRecBytes = 32;   // unfiltered bottom row: Y 16, U 8, V 8 (intra prediction)

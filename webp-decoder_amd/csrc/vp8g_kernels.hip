@@ -45,9 +45,17 @@ __device__ unsigned long long g_vp8g_wave_times[64];  // frame 0: per wave {star
 		st_acc[i] += t_ - st_prev;                        \
 		st_prev = t_;                                     \
 	} while (0)
+#elif defined(VP8G_MARKS)
+#define STAMP(i) asm volatile(";MARK_" #i)  // static per-phase instruction counts (tools/section_counts.py)
+#define SUBMARK(i) asm volatile(";MARK_" #i)
 #else
 #define STAMP(i) \
 	do {         \
+	} while (0)
+#endif
+#ifndef SUBMARK
+#define SUBMARK(i) \
+	do {           \
 	} while (0)
 #endif
 
@@ -58,42 +66,63 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 // ---------------------------------------------------------------------------------------------
-// B_PRED predictor table (RFC 6386 12.3; reference vp8_recon.c:218-358).  Edge array bytes in
-// LDS: [0..3] = L3 L2 L1 L0, [7] = P (corner), [8..15] = A0..A7.  Entry = 3 byte positions +
-// kind (0 avg3, 1 avg2, 2 copy).  Modes 0 (DC) and 1 (TM) are computed directly.
+// B_PRED predictor table (RFC 6386 12.3; reference vp8_recon.c:218-358).  A lane predicting one
+// pixel of a 4x4 sub-block holds the sub-block's edge as 16 bytes E: [0..3] = L0..L3 (left
+// column, top down), [4..6] = 128, [7] = P (corner), [8..15] = A0..A7 (above + above-right).
+// Every directional mode is avg3(x, y, z) = (x + 2y + z + 2) >> 2 of three edge bytes (avg2(x, y)
+// = avg3(x, y, x), a copy = avg3(x, x, x)), so an entry is just three byte positions, stored
+// as v_perm selectors (pos & 7) plus a byte mask picking the high half (pos >= 8) of E: one
+// perm pair + one bfi fetches all three, one v_dot4_u32_u8 weighs them.  TM_PRED keeps its own
+// formula sat8(L + A - P) over the entry's positions (L_r, P, A_c); DC_PRED is a direct sum.
+// Entry kBpModes-1 (all positions 128) serves out-of-range modes.
+// Edge index notation of the builders: 0..3 = L3..L0, 4 = P, 5..12 = A0..A7.
 // ---------------------------------------------------------------------------------------------
 struct BpTab {
-	uint16_t v[256];
+	uint32_t v[kBpModes * 16 * 2];
 };
-constexpr int epos(int e) { return e < 4 ? e : (e == 4 ? 7 : e + 3); }
-constexpr uint16_t ent(int kind, int a, int b, int c) {
-	return (uint16_t)(epos(a) | (epos(b) << 4) | (epos(c) << 8) | (kind << 12));
-}
-constexpr uint16_t A3(int a, int b, int c) { return ent(0, a, b, c); }
-constexpr uint16_t A2(int a, int b) { return ent(1, a, b, b); }
-constexpr uint16_t CP(int a) { return ent(2, a, a, a); }
+constexpr int epos(int e) { return e < 4 ? 3 - e : (e == 4 ? 7 : e + 3); }
+struct Tri {
+	int a, b, c;  // byte positions in E
+};
+constexpr Tri A3(int a, int b, int c) { return Tri{epos(a), epos(b), epos(c)}; }
+constexpr Tri A2(int a, int b) { return Tri{epos(a), epos(b), epos(a)}; }
+constexpr Tri CP(int a) { return Tri{epos(a), epos(a), epos(a)}; }
 
 constexpr BpTab make_bptab() {
 	BpTab t{};
-	const uint16_t vr[16] = {A2(4, 5), A2(5, 6), A2(6, 7), A2(7, 8), A3(3, 4, 5), A3(4, 5, 6), A3(5, 6, 7), A3(6, 7, 8),
-	                         A3(2, 3, 4), A2(4, 5), A2(5, 6), A2(6, 7), A3(1, 2, 3), A3(3, 4, 5), A3(4, 5, 6), A3(5, 6, 7)};
-	const uint16_t vl[16] = {A2(5, 6), A2(6, 7), A2(7, 8), A2(8, 9), A3(5, 6, 7), A3(6, 7, 8), A3(7, 8, 9), A3(8, 9, 10),
-	                         A2(6, 7), A2(7, 8), A2(8, 9), A3(9, 10, 11), A3(6, 7, 8), A3(7, 8, 9), A3(8, 9, 10), A3(10, 11, 12)};
-	const uint16_t hd[16] = {A2(3, 4), A3(3, 4, 5), A3(4, 5, 6), A3(5, 6, 7), A2(2, 3), A3(2, 3, 4), A2(3, 4), A3(3, 4, 5),
-	                         A2(1, 2), A3(1, 2, 3), A2(2, 3), A3(2, 3, 4), A2(0, 1), A3(0, 1, 2), A2(1, 2), A3(1, 2, 3)};
-	const uint16_t hu[16] = {A2(3, 2), A3(3, 2, 1), A2(2, 1), A3(2, 1, 0), A2(2, 1), A3(2, 1, 0), A2(1, 0), A3(1, 0, 0),
-	                         A2(1, 0), A3(1, 0, 0), CP(0), CP(0), CP(0), CP(0), CP(0), CP(0)};
-	for (int p = 0; p < 16; p++) {
-		const int r = p >> 2, c = p & 3;
-		t.v[2 * 16 + p] = A3(4 + c, 5 + c, 6 + c);                                        // B_VE
-		t.v[3 * 16 + p] = r == 3 ? A3(1, 0, 0) : A3(4 - r, 3 - r, 2 - r);                 // B_HE
-		t.v[4 * 16 + p] = A3(5 + r + c, 6 + r + c, (7 + r + c) > 12 ? 12 : (7 + r + c));  // B_LD
-		t.v[5 * 16 + p] = A3(3 - r + c, 4 - r + c, 5 - r + c);                            // B_RD
-		t.v[6 * 16 + p] = vr[p];
-		t.v[7 * 16 + p] = vl[p];
-		t.v[8 * 16 + p] = hd[p];
-		t.v[9 * 16 + p] = hu[p];
-	}
+	const Tri vr[16] = {A2(4, 5), A2(5, 6), A2(6, 7), A2(7, 8), A3(3, 4, 5), A3(4, 5, 6), A3(5, 6, 7), A3(6, 7, 8),
+	                    A3(2, 3, 4), A2(4, 5), A2(5, 6), A2(6, 7), A3(1, 2, 3), A3(3, 4, 5), A3(4, 5, 6), A3(5, 6, 7)};
+	const Tri vl[16] = {A2(5, 6), A2(6, 7), A2(7, 8), A2(8, 9), A3(5, 6, 7), A3(6, 7, 8), A3(7, 8, 9), A3(8, 9, 10),
+	                    A2(6, 7), A2(7, 8), A2(8, 9), A3(9, 10, 11), A3(6, 7, 8), A3(7, 8, 9), A3(8, 9, 10), A3(10, 11, 12)};
+	const Tri hd[16] = {A2(3, 4), A3(3, 4, 5), A3(4, 5, 6), A3(5, 6, 7), A2(2, 3), A3(2, 3, 4), A2(3, 4), A3(3, 4, 5),
+	                    A2(1, 2), A3(1, 2, 3), A2(2, 3), A3(2, 3, 4), A2(0, 1), A3(0, 1, 2), A2(1, 2), A3(1, 2, 3)};
+	const Tri hu[16] = {A2(3, 2), A3(3, 2, 1), A2(2, 1), A3(2, 1, 0), A2(2, 1), A3(2, 1, 0), A2(1, 0), A3(1, 0, 0),
+	                    A2(1, 0), A3(1, 0, 0), CP(0), CP(0), CP(0), CP(0), CP(0), CP(0)};
+	for (int m = 0; m < kBpModes; m++)
+		for (int p = 0; p < 16; p++) {
+			const int r = p >> 2, c = p & 3;
+			Tri e{4, 4, 4};  // 128 (DC_PRED is computed directly; out-of-range modes)
+			switch (m) {
+				case 1: e = Tri{r, 7, 8 + c}; break;                                      // B_TM: L_r, P, A_c
+				case 2: e = A3(4 + c, 5 + c, 6 + c); break;                               // B_VE
+				case 3: e = r == 3 ? A3(1, 0, 0) : A3(4 - r, 3 - r, 2 - r); break;        // B_HE
+				case 4: e = A3(5 + r + c, 6 + r + c, (7 + r + c) > 12 ? 12 : (7 + r + c)); break;  // B_LD
+				case 5: e = A3(3 - r + c, 4 - r + c, 5 - r + c); break;                   // B_RD
+				case 6: e = vr[p]; break;
+				case 7: e = vl[p]; break;
+				case 8: e = hd[p]; break;
+				case 9: e = hu[p]; break;
+				default: break;
+			}
+			const int pos[3] = {e.a, e.b, e.c};
+			uint32_t sel = 12u << 24, mask = 0;  // byte 3: constant 0
+			for (int k = 0; k < 3; k++) {
+				sel |= (uint32_t)(pos[k] & 7) << (8 * k);
+				if (pos[k] >= 8) mask |= 0xFFu << (8 * k);
+			}
+			t.v[(m * 16 + p) * 2] = sel;
+			t.v[(m * 16 + p) * 2 + 1] = mask;
+		}
 	return t;
 }
 __constant__ BpTab kBpTab = make_bptab();
@@ -164,13 +193,6 @@ DEV uint32_t pack4(int a, int b, int c, int d) {
 }
 DEV int ubyte(uint32_t w, int i) { return (int)((w >> (8 * i)) & 0xFFu); }
 DEV uint32_t lo16(int a, int b) { return (uint32_t)(a & 0xFFFF) | ((uint32_t)b << 16); }
-// byte q (0..15) of a 16-byte value held in 4 dwords
-DEV int byte16(u32x4 d, int q) {
-	const uint32_t sel = (uint32_t)(q & 7) * 0x01010101u;
-	const uint32_t lo = __builtin_amdgcn_perm(d.y, d.x, sel);
-	const uint32_t hi = __builtin_amdgcn_perm(d.w, d.z, sel);
-	return (int)(((q & 8) ? hi : lo) & 0xFFu);
-}
 DEV int rdlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 
 // Per-frame context (unfiltered bottom rows + filter-state bottom rows per MB column), in LDS
@@ -348,7 +370,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 	const uint32_t f = blockIdx.x;
 	const Vp8gFrameDesc& D = descs[f];
 
-	for (int i = (int)threadIdx.x; i < 256; i += NW * 64) ((uint16_t*)(smem + kBpTable))[i] = kBpTab.v[i];
+	for (int i = (int)threadIdx.x; i < kBpModes * 32; i += NW * 64) ((uint32_t*)(smem + kBpTable))[i] = kBpTab.v[i];
 	for (int i = (int)threadIdx.x; i < 96; i += NW * 64) ((uint16_t*)(smem + kFlushTable))[i] = kFlushTab.v[i];
 	if (threadIdx.x < 24) ((int16_t*)(smem + kDqTable))[threadIdx.x] = D.dq[threadIdx.x / 6][threadIdx.x % 6];
 	if (threadIdx.x < 32) smem[kLfTable + threadIdx.x] = D.lf[threadIdx.x >> 3][(threadIdx.x >> 2) & 1][threadIdx.x & 3];
@@ -561,34 +583,32 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 						const uint8_t* s = src + (p ? D.src_v : D.src_u) + (size_t)(cy0 + row) * D.src_stride_uv + cx0;
 						st64((p ? tV : tU) + (4 + row) * 16 + slot * 8, u32x2{ld32(s), ld32(s + 4)});
 					}
-				} else if (ln < 4) {  // luma above row
-					st32(abY + 16 + 4 * ln, top ? 0x7F7F7F7Fu : ctx.rd(rec_off(cu) + 4 * ln));
-				} else if (ln == 4) {  // luma above-right (row above the MB, cols x+16..x+19)
-					uint32_t v4;
-					if (top) v4 = 0x7F7F7F7Fu;
-					else if (cu + 1 < C) v4 = ctx.rd(rec_off(cu + 1));
-					else v4 = (ctx.rd(rec_off(cu) + 12) >> 24) * 0x01010101u;  // clamp to padded width
-					st32(abY + 32, v4);
-				} else if (ln < 9) {  // chroma above rows
-					const int q = ln - 5, p = q >> 1, dw = q & 1;
-					st32(abUV + 16 * p + 8 + 4 * dw, top ? 0x7F7F7F7Fu : ctx.rd(rec_off(cu) + 16 + 8 * p + 4 * dw));
-				} else if (ln < 17) {  // left columns at the frame's left edge: 129
-					if (c == 0) st32(left + 4 * (ln - 9), 0x81818181u);
-				} else if (ln == 17) {  // corners at the left edge: 127 on the top row, else 129
-					if (c == 0) {
-						const uint8_t pv = top ? 127 : 129;
-						abY[15] = pv;
-						abUV[7] = pv;
-						abUV[23] = pv;
-					}
+				} else {
+					// ln 0..3 luma above row, 4 luma above-right (cols x+16..x+19, clamped to the
+					// padded width in the last column), 5..8 chroma above rows; 9..16 left columns at
+					// the frame's left edge (129); 17..19 corners there (127 on the top row, else 129);
+					// 20..31 the filter state of the MB above (luma 4 x 16 B, chroma 8 x 8 B).
+					const bool ar = ln == 4;
+					const bool clampc = ar && cu + 1 == C;
+					const int q = ln - 5;
+					const uint32_t soff = ln < 4 ? rec_off(cu) + 4 * ln
+					                             : (ar ? (clampc ? rec_off(cu) + 12 : rec_off(cu + 1))
+					                                   : rec_off(cu) + 16 + 8 * (q >> 1) + 4 * (q & 1));
+					uint8_t* const dst32 = ln < 4 ? abY + 16 + 4 * ln
+					                              : (ar ? abY + 32 : (ln < 9 ? abUV + 8 + 16 * (q >> 1) + 4 * (q & 1) : left + 4 * (ln - 9)));
+					uint32_t v = 0x81818181u;
+					if (ln < 9) v = top ? 0x7F7F7F7Fu : ctx.rd(soff);
+					if (clampc && !top) v = (v >> 24) * 0x01010101u;
+					if (ln < 9 || (ln < 17 && c == 0)) st32(dst32, v);
+					if (ln >= 17 && ln < 20 && c == 0) (ln == 17 ? abY + 15 : abUV + 7 + 16 * (ln - 18))[0] = top ? 127 : 129;
 				}
-				if (lf_on && !top && ln >= 18 && ln < 30) {  // filter state of the MB above
-					if (ln < 22) {
-						st128(tY + (ln - 18) * 32 + slot * 16, ctx.rd128(lf_off(cu) + (ln - 18) * 16));
-					} else {
-						const int p = (ln - 22) >> 2, tr = (ln - 22) & 3;
-						st64((p ? tV : tU) + tr * 16 + slot * 8, ctx.rd64(lf_off(cu) + 64 + p * 32 + tr * 8));
-					}
+				if (lf_on && !top && ln >= 20) {  // filter state of the MB above (both modes)
+					const bool ly = ln < 24;
+					const int p = (ln - 24) >> 2, tr = ly ? ln - 20 : (ln - 24) & 3;
+					const uint32_t lo = lf_off(cu) + (ly ? tr * 16 : 64 + p * 32 + tr * 8);
+					uint8_t* const td = ly ? tY + tr * 32 + slot * 16 : (p ? tV : tU) + tr * 16 + slot * 8;
+					st64(td, ctx.rd64(lo));
+					if (ly) st64(td + 8, ctx.rd64(lo + 8));
 				}
 			}
 			wave_lds_sync();
@@ -596,10 +616,10 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 
 			// ---------------------------------------------- prediction + reconstruction
 			if (!lf_only) {
-				const bool have_above = r > 0, have_left = c > 0;
 				if (act && ln < 24 && (ln >= 16 || !bpred)) {
 					// whole-block predictors (RFC 12.2; reference vp8_recon.c:152-212, 533-560, 605-651),
-					// one 4x4 block per lane
+					// one 4x4 block per lane, branch-free: every mode is sat8(L' + A' + K) with
+					// L' = L & mL, A' = A & mA (DC: K = dc value; V: mA; H: mL; TM: both, K = -P)
 					const bool yl = ln < 16;
 					const int p = (ln - 16) >> 2;  // chroma plane (chroma lanes)
 					const int blk = yl ? ln : (ln & 3);
@@ -607,86 +627,101 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					const uint8_t* ab = yl ? abY + 16 : abUV + 16 * p + 8;
 					const uint8_t* lc = yl ? left : left + 16 + 8 * p;
 					const int mode = yl ? (ymode > 4 ? 0 : ymode) : (uvmode > 3 ? 0 : uvmode);
-					int dcv = 128;
-					{
-						uint32_t sa = bsum4(ld32(ab)) + bsum4(ld32(ab + 4));
-						uint32_t sl = bsum4(ld32(lc)) + bsum4(ld32(lc + 4));
-						if (yl) {
-							sa += bsum4(ld32(ab + 8)) + bsum4(ld32(ab + 12));
-							sl += bsum4(ld32(lc + 8)) + bsum4(ld32(lc + 12));
-						}
-						const int sh = yl ? 4 : 3;
-						if (have_above && have_left) dcv = (int)(sa + sl + (1u << sh)) >> (sh + 1);
-						else if (have_left) dcv = (int)(sl + (1u << (sh - 1))) >> sh;
-						else if (have_above) dcv = (int)(sa + (1u << (sh - 1))) >> sh;
-					}
+					const u32x2 a01 = ld64(ab), a23 = ld64(ab + 8), l01 = ld64(lc), l23 = ld64(lc + 8);
+					const uint32_t sa2 = __builtin_amdgcn_sad_u8(a01.y, 0u, __builtin_amdgcn_sad_u8(a01.x, 0u, 0u));
+					const uint32_t sl2 = __builtin_amdgcn_sad_u8(l01.y, 0u, __builtin_amdgcn_sad_u8(l01.x, 0u, 0u));
+					const uint32_t sa4 = __builtin_amdgcn_sad_u8(a23.y, 0u, __builtin_amdgcn_sad_u8(a23.x, 0u, sa2));
+					const uint32_t sl4 = __builtin_amdgcn_sad_u8(l23.y, 0u, __builtin_amdgcn_sad_u8(l23.x, 0u, sl2));
+					const bool ha = r > 0, hl = c > 0;
+					const uint32_t sum = (ha ? (yl ? sa4 : sa2) : 0u) + (hl ? (yl ? sl4 : sl2) : 0u);
+					const int shift = (yl ? 3 : 2) + (ha ? 1 : 0) + (hl ? 1 : 0);  // 16 or 8 samples per edge
+					const int dcv = (ha || hl) ? (int)((sum + (1u << (shift - 1))) >> shift) : 128;
 					const uint32_t aw = ld32(ab + 4 * bx);
 					const uint32_t lw = ld32(lc + 4 * by);
 					const int P = (int)ab[-1];
+					const uint32_t mA = (mode == 1 || mode == 3) ? 0xFFu : 0u;
+					const uint32_t mL = (mode == 2 || mode == 3) ? 0xFFu : 0u;
+					const int K = (mode == 3 ? -P : 0) + (mode == 0 ? dcv : 0);
 					uint8_t* dst = yl ? tY + (4 + 4 * by) * 32 + slot * 16 + 4 * bx
 					                  : (p ? tV : tU) + (4 + 4 * by) * 16 + slot * 8 + 4 * bx;
 					const int dstride = yl ? 32 : 16;
 					const u32x4 r01 = ld128(hv + kResid + ln * 32), r23 = ld128(hv + kResid + ln * 32 + 16);
 					const uint32_t rw[8] = {r01.x, r01.y, r01.z, r01.w, r23.x, r23.y, r23.z, r23.w};
+					int acol[4];
+#pragma unroll
+					for (int cc = 0; cc < 4; cc++) acol[cc] = (int)((aw >> (8 * cc)) & mA) + K;
 #pragma unroll
 					for (int rr = 0; rr < 4; rr++) {
-						const int L = ubyte(lw, rr);
+						const int L = (int)((lw >> (8 * rr)) & mL);
 						int px4[4];
 #pragma unroll
 						for (int cc = 0; cc < 4; cc++) {
-							const int a = ubyte(aw, cc);
-							const int pred = mode == 1 ? a : (mode == 2 ? L : (mode == 3 ? sat8(L + a - P) : dcv));
 							const int rv = (int)(int16_t)((rw[(4 * rr + cc) >> 1] >> (16 * (cc & 1))) & 0xFFFFu);
-							px4[cc] = sat8(pred + rv);
+							px4[cc] = sat8(sat8(L + acol[cc]) + rv);
 						}
 						st32(dst + rr * dstride, pack4(px4[0], px4[1], px4[2], px4[3]));
 					}
 				}
 				wave_lds_sync();
+				SUBMARK(20);
 				const bool bp_lane = act && bpred;
 				if (__ballot(bp_lane) != 0ull && !(VP8G_ABLATE & 2)) {
-					// B_PRED: 16 sub-blocks along the 2i+j wavefront (10 steps, <= 2 sub-blocks
-					// each), using already reconstructed pixels (reference vp8_recon.c:454-530)
+					// B_PRED: 16 sub-blocks along the 2i+j wavefront (10 steps, <= 2 sub-blocks each;
+					// lanes 0..15 / 16..31 of a half = group g take sub-block (i0 + g, s - 2 i0 - 2 g)),
+					// one pixel per lane, from already reconstructed pixels (reference
+					// vp8_recon.c:454-530).  Fully unrolled: every per-step offset is a constant, the
+					// per-lane parts are hoisted.  Edge sources (reference vp8_recon.c:464-504): the row
+					// above is the MB's above row when i == 0 and the tile otherwise, A4..A7 of the
+					// last sub-block column come from the MB above (abY + 32), the left column of
+					// sub-block column j is at kLeft - 16 j (kColY, written here by the lanes of
+					// pixel column 3), P is the byte before the above row (i == 0) or the left column.
 					const u32x4 bm0 = u32x4{(uint32_t)rdlane((int)cur.a.x, 25), (uint32_t)rdlane((int)cur.a.y, 25),
 					                        (uint32_t)rdlane((int)cur.a.z, 25), (uint32_t)rdlane((int)cur.a.w, 25)};
 					const u32x4 bm1 = u32x4{(uint32_t)rdlane((int)cur.a.x, 57), (uint32_t)rdlane((int)cur.a.y, 57),
 					                        (uint32_t)rdlane((int)cur.a.z, 57), (uint32_t)rdlane((int)cur.a.w, 57)};
 					const u32x4 bmw = hh ? bm1 : bm0;
-					const int g = (ln >> 4) & 1, p = ln & 15;
-					const int16_t* rs = (const int16_t*)(hv + kResid);
-					const uint16_t* bptab = (const uint16_t*)(smem + kBpTable);
+					const int g = (ln >> 4) & 1, p = ln & 15, rr = p >> 2, cc = p & 3;
+					uint8_t* const tpix = tY + slot * 16 + 4 * 32 + 120 * g + 32 * rr + cc;  // + 120 i0 + 4 s
+					const uint8_t* const tA = tY + slot * 16 + 3 * 32 + 120 * g;             // + 120 i0 + 4 s
+					const uint8_t* const aE = g ? tA : abY + 16;                              // i0 == 0: + 4 s
+					uint8_t* const lB = left + 36 * g;                                        // + 36 i0 - 16 s
+					const int16_t* const rsp = (const int16_t*)(hv + kResid) + p + 32 * g;    // + 16 b0
+					const u32x2* const tabp = (const u32x2*)(smem + kBpTable) + p;            // + 16 mode
+					const bool col3 = cc == 3;
+#pragma unroll
 					for (int s = 0; s < 10; s++) {
-						const int ilo = s <= 3 ? 0 : (s - 2) >> 1;
-						const int i = ilo + g, j = s - 2 * i;
-						if (bp_lane && i <= 3 && j >= 0 && j <= 3) {
-							// Each pixel lane assembles the sub-block's 13 edge pixels itself (one LDS round
-							// trip): edge rules of reference vp8_recon.c:464-504 -- the row above is the MB's
-							// above row when i == 0, the left column the MB's left column when j == 0, and
-							// the above-right of the last sub-block column always comes from the MB above.
-							const int b = 4 * i + j;
-							const int mode = byte16(bmw, b);
-							const int rr = p >> 2, cc = p & 3;
-							const uint8_t* arow = (i == 0) ? abY + 16 : tY + (3 + 4 * i) * 32 + slot * 16;
-							const uint32_t a03 = ld32(arow + 4 * j);
-							const uint32_t a47 = ld32(j == 3 ? abY + 32 : arow + 4 * j + 4);
-							const uint8_t* lcol = (j == 0) ? left + 4 * i : tY + (4 + 4 * i) * 32 + slot * 16 + 4 * j - 1;
-							const int ls = (j == 0) ? 1 : 32;
-							const uint32_t l0 = lcol[0], l1 = lcol[ls], l2 = lcol[2 * ls], l3 = lcol[3 * ls];
-							const uint8_t* pp = (i == 0) ? abY + 15 + 4 * j
-							                             : ((j == 0) ? left + 4 * i - 1 : tY + (3 + 4 * i) * 32 + slot * 16 + 4 * j - 1);
+						const int i0 = s <= 3 ? 0 : (s - 2) >> 1;
+						const int j0 = s - 2 * i0;  // g = 0: (i0, j0); g = 1: (i0 + 1, j0 - 2)
+						const bool v0 = j0 <= 3, v1 = i0 + 1 <= 3 && j0 >= 2;
+						const bool valid = bp_lane && (g ? v1 : v0);
+						if (valid) {
+							const int b0 = 4 * i0 + j0;
+							const int mb0 = v0 ? (int)((bmw[b0 >> 2] >> (8 * (b0 & 3))) & 0xFFu) : 0;
+							const int mb1 = v1 ? (int)((bmw[(b0 + 2) >> 2] >> (8 * ((b0 + 2) & 3))) & 0xFFu) : 0;
+							const int mode = min(g ? mb1 : mb0, kBpModes - 1);
+							const uint8_t* const arow = i0 == 0 ? aE + 4 * s : tA + 120 * i0 + 4 * s;
+							// above-right: the MB above's row when this sub-block is in column 3
+							const bool r3_0 = j0 == 3, r3_1 = j0 == 5;
+							const uint8_t* const a47p = (r3_0 || r3_1) ? ((g ? r3_1 : r3_0) ? abY + 32 : arow + 4) : arow + 4;
+							uint8_t* const lb = lB + 36 * i0 - 16 * s;
+							const uint8_t* const pp = i0 == 0 ? (g ? lb - 1 : arow - 1) : lb - 1;
+							const uint32_t a03 = ld32(arow), a47 = ld32(a47p), lw = ld32(lb);
 							const uint32_t pv = *pp;
-							const uint32_t tb = bptab[(mode & 15) * 16 + p];
-							const int rv = rs[b * 16 + p];
-							const u32x4 E = u32x4{l3 | (l2 << 8) | (l1 << 16) | (l0 << 24), pv << 24, a03, a47};
-							const int xa = byte16(E, (int)(tb & 15));
-							const int xb = byte16(E, (int)((tb >> 4) & 15));
-							const int xc = byte16(E, (int)((tb >> 8) & 15));
-							const uint32_t kind = tb >> 12;
-							const int vt = kind == 0 ? (xa + 2 * xb + xc + 2) >> 2 : (kind == 1 ? (xa + xb + 1) >> 1 : xa);
-							const int vdc = (int)(bsum4(E.x) + bsum4(E.z) + 4) >> 3;
-							const int vtm = sat8((int)ubyte(E.x, 3 - rr) + (int)ubyte(a03, cc) - (int)pv);
-							const int pred = mode == 0 ? vdc : (mode == 1 ? vtm : (mode <= 9 ? vt : 128));
-							tY[(4 + 4 * i + rr) * 32 + slot * 16 + 4 * j + cc] = (uint8_t)sat8(pred + rv);
+							const u32x2 tb = tabp[16 * mode];
+							const int rv = rsp[16 * b0];
+							const uint32_t ey = (pv << 24) | 0x808080u;
+							const uint32_t lo = __builtin_amdgcn_perm(ey, lw, tb.x);
+							const uint32_t hi = __builtin_amdgcn_perm(a47, a03, tb.x);
+							const uint32_t x3 = (hi & tb.y) | (lo & ~tb.y);  // bytes 0..2 = x, y, z
+							const int vt = (int)(__builtin_amdgcn_udot4(x3, 0x00010201u, 2u, false) >> 2);
+							const int vtm = sat8((int)__builtin_amdgcn_udot4(x3, 0x00010001u, 0u, false) - (int)((x3 >> 8) & 0xFFu));
+							const int vdc = (int)((__builtin_amdgcn_sad_u8(a03, 0u, __builtin_amdgcn_sad_u8(lw, 0u, 4u))) >> 3);
+							const int pred = mode == 0 ? vdc : (mode == 1 ? vtm : vt);
+							const int px = sat8(pred + rv);
+							tpix[120 * i0 + 4 * s] = (uint8_t)px;
+							// right pixel column of a sub-block: left column of the next sub-block column
+							const bool w3 = (g ? j0 - 2 : j0) < 3;
+							if (col3 && w3) lb[-16 + rr] = (uint8_t)px;
 						}
 						wave_lds_sync();
 					}
@@ -728,29 +763,34 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			STAMP(5);
 
 			// ---------------------------------------------- store final pixels
-			// crop-aware store of an 8- or 16-byte row piece from LDS
-			auto put = [&](uint8_t* plane, uint32_t stride, uint32_t vis_w, uint32_t vis_h, uint32_t row, uint32_t col,
-			               const uint8_t* src, bool w16) {
-				if (row >= vis_h || col >= vis_w || (VP8G_ABLATE & 4)) return;
-				uint8_t* d = plane + (size_t)row * stride + col;
-				const uint32_t n = vis_w - col, wdt = w16 ? 16u : 8u;
-				if (n >= wdt && (((uintptr_t)d) & (wdt - 1)) == 0) {
-					if (w16) *(u32x4*)d = ld128(src);
-					else *(u32x2*)d = ld64(src);
-				} else {
-					const uint32_t cnt = n < wdt ? n : wdt;
-					for (uint32_t q = 0; q < cnt; q++) d[q] = src[q];
+			// One row piece per lane (luma 16 B, chroma 8 B) from LDS to the output plane or, for the
+			// bottom rows the next MB row still filters, to ctx_lf.  Straight-line: the crop / odd
+			// alignment case (a partial row piece at the right edge) is a rare wave-uniform branch.
+			auto emit = [&](bool ok, int pl, uint32_t prow, uint32_t col, const uint8_t* src) {
+				const bool isy = pl == 0;
+				const u32x2 lo = ld64(src), hi = ld64(src + 8);  // hi: luma only
+				const uint32_t colpx = col * (isy ? 16u : 8u), nb = isy ? 16u : 8u;
+				uint8_t* const plane = isy ? outY : (pl == 2 ? outV : outU);
+				uint8_t* const d = plane + (size_t)prow * (isy ? sy : suv) + colpx;
+				const bool vis = ok && prow < (isy ? H : CH) && !(VP8G_ABLATE & 4);
+				const uint32_t vw = isy ? W : CW;
+				const bool full = colpx + nb <= vw && (((uintptr_t)d) & (nb - 1)) == 0;
+				if (vis && full) {
+					if (isy) *(u32x4*)d = u32x4{lo.x, lo.y, hi.x, hi.y};
+					else *(u32x2*)d = lo;
+				}
+				if (__ballot(vis && !full) != 0ull) {
+					if (vis && !full) {
+						const uint32_t n = vw - colpx, cnt = n < nb ? n : nb;
+						for (uint32_t q = 0; q < cnt; q++) d[q] = src[q];
+					}
 				}
 			};
 			if (!lf_on) {
 				// unfiltered: MB(r, c) is final as soon as it is reconstructed
-				if (act) {
-					if (ln < 16) put(outY, sy, W, H, y0 + ln, x0, tY + (4 + ln) * 32 + slot * 16, true);
-					else {
-						const int p = (ln - 16) >> 3, row = ln & 7;
-						put(p ? outV : outU, suv, CW, CH, cy0 + row, cx0, (p ? tV : tU) + (4 + row) * 16 + slot * 8, false);
-					}
-				}
+				const int pl = ln < 16 ? 0 : ((ln - 16) >> 3) + 1, row = ln < 16 ? ln : (ln & 7);
+				const uint8_t* src = ln < 16 ? tY + (4 + ln) * 32 + slot * 16 : (pl == 2 ? tV : tU) + (4 + row) * 16 + slot * 8;
+				emit(act, pl, (ln < 16 ? y0 : cy0) + row, cu, src);
 			} else {
 				const bool last_row = r + 1 == R;
 				const bool last_col = cu + 1 == C;
@@ -760,21 +800,19 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					const uint32_t e = ftab[rd * 32 + ln];
 					const int pl = (e >> 8) & 3, kind = (e >> 6) & 3, prev = (e >> 5) & 1, kk = e & 15;
 					const bool ok = act && (e & 0x8000u) && (kind != 0 || r > 0) && (prev ? c > 0 : (kind == 0 || last_col));
-					if (ok) {
-						const uint32_t col = prev ? cu - 1 : cu;
-						const int sl = prev ? slot ^ 1 : slot;
-						if (pl == 0) {
-							const int trow = kind == 0 ? kk : (kind == 1 ? 4 + kk : 16 + kk);
-							const uint8_t* src = tY + trow * 32 + sl * 16;
-							if (kind == 2 && !last_row) ctx.wr128(lf_off(col) + kk * 16, ld128(src));
-							else put(outY, sy, W, H, kind == 0 ? y0 - 4 + kk : y0 + trow - 4, col * 16, src, true);
-						} else {
-							const int trow = kind == 0 ? kk : (kind == 1 ? 4 + kk : 8 + kk);
-							const uint8_t* src = (pl == 2 ? tV : tU) + trow * 16 + sl * 8;
-							if (kind == 2 && !last_row) ctx.wr64(lf_off(col) + 64 + (pl - 1) * 32 + kk * 8, ld64(src));
-							else put(pl == 2 ? outV : outU, suv, CW, CH, kind == 0 ? cy0 - 4 + kk : cy0 + trow - 4, col * 8, src, false);
-						}
+					const bool isy = pl == 0;
+					const uint32_t col = prev ? cu - 1 : cu;
+					const int sl = slot ^ prev;
+					// tile row: top strip 0..3, body 4.., tail 16.. (luma) / 8.. (chroma); image row = base + trow - 4
+					const int trow = kind == 0 ? kk : (kind == 1 ? 4 + kk : (isy ? 16 : 8) + kk);
+					const uint8_t* src = isy ? tY + trow * 32 + sl * 16 : (pl == 2 ? tV : tU) + trow * 16 + sl * 8;
+					const bool to_ctx = ok && kind == 2 && !last_row;
+					if (to_ctx) {
+						const uint32_t off = lf_off(col) + (isy ? kk * 16 : 64 + (pl - 1) * 32 + kk * 8);
+						ctx.wr64(off, ld64(src));
+						if (isy) ctx.wr64(off + 8, ld64(src + 8));
 					}
+					emit(ok && !to_ctx, pl, (isy ? y0 : cy0) + trow - 4, col, src);
 				}
 			}
 			wave_lds_sync();
