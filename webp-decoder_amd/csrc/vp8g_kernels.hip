@@ -193,6 +193,22 @@ DEV uint32_t pack4(int a, int b, int c, int d) {
 }
 DEV int ubyte(uint32_t w, int i) { return (int)((w >> (8 * i)) & 0xFFu); }
 DEV uint32_t lo16(int a, int b) { return (uint32_t)(a & 0xFFFF) | ((uint32_t)b << 16); }
+// packed int16 pairs (wrapping, as the reference's int16 stores)
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+DEV u16x2 as_p(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
+DEV uint32_t as_w(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+DEV uint32_t pk_add(uint32_t a, uint32_t b) { return as_w(as_p(a) + as_p(b)); }
+DEV uint32_t pk_sub(uint32_t a, uint32_t b) { return as_w(as_p(a) - as_p(b)); }
+DEV uint32_t pk_mul(uint32_t a, uint32_t b) { return as_w(as_p(a) * as_p(b)); }
+DEV int lo_s16(uint32_t x) { return (int)(int16_t)(x & 0xFFFFu); }
+DEV int hi_s16(uint32_t x) { return (int)(int16_t)(x >> 16); }
+DEV uint32_t pack2(int a, int b) { return __builtin_amdgcn_perm((uint32_t)b, (uint32_t)a, 0x05040100u); }
+// floor(x * c / 65536) of each int16 half
+DEV uint32_t mulhi2(uint32_t x, int c) {
+	return __builtin_amdgcn_perm((uint32_t)(hi_s16(x) * c), (uint32_t)(lo_s16(x) * c), 0x07060302u);
+}
+DEV uint32_t mul_s2(uint32_t x) { return pk_add(x, mulhi2(x, 35468 - 65536)); }  // mul_s of both halves, mod 2^16
+DEV uint32_t mul_c2(uint32_t x) { return pk_add(x, mulhi2(x, 20091)); }
 DEV int rdlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 
 // Per-frame context (unfiltered bottom rows + filter-state bottom rows per MB column), in LDS
@@ -402,30 +418,29 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 #endif
 
 	// Loads for one lane of one step: coefficient blocks (ln 0..24), bmode (25), side bytes (26..29).
+	// Straight-line: every lane issues the same three loads; lanes without a role (and halves
+	// outside the frame, which read MB mb0) load duplicate addresses and ignore the result.
 	auto prefetch = [&](int lane, uint32_t rA, bool two, int tt) -> Pref {
 		Pref p;
-		p.a = u32x4{0u, 0u, 0u, 0u};
-		p.b = p.a;
-		p.side = 0;
 		const int hh = lane >> 5, ln = lane & 31;
 		const int cn = tt - 2 * hh;
-		if ((hh == 0 || two) && cn >= 0 && cn < (int)C) {
-			const uint64_t m = mb0 + (uint64_t)(rA + hh) * C + (uint32_t)cn;
-			if (ln < 25) {
-				const int16_t* src = ln < 16 ? A.coeff_y + (m * 16 + ln) * 16
-				                             : (ln < 20 ? A.coeff_u + (m * 4 + ln - 16) * 16
-				                                        : (ln < 24 ? A.coeff_v + (m * 4 + ln - 20) * 16 : A.coeff_y2 + m * 16));
-				if (!lf_only) {
-					p.a = __builtin_nontemporal_load((const u32x4*)src);
-					p.b = __builtin_nontemporal_load((const u32x4*)src + 1);
-				}
-			} else if (ln == 25) {
-				if (!lf_only) p.a = *(const u32x4*)(A.bmode + m * 16);
-			} else if (ln < 30) {
-				const uint8_t* sp = ln == 26 ? A.ymode : (ln == 27 ? A.uv_mode : (ln == 28 ? A.segment_id : A.has_coeff));
-				p.side = sp[m];
-			}
+		const bool inb = (hh == 0 || two) && cn >= 0 && cn < (int)C;
+		const uint64_t m = mb0 + (inb ? (uint64_t)((rA + hh) * C + (uint32_t)cn) : 0ull);
+		if (!lf_only) {
+			const bool isb = ln == 25;
+			const uint64_t idx = ln < 16 ? m * 16 + ln : (ln < 24 ? m * 4 + (ln & 3) : m);
+			const uint8_t* base = ln < 16 ? (const uint8_t*)A.coeff_y
+			                              : (ln < 20 ? (const uint8_t*)A.coeff_u : (ln < 24 ? (const uint8_t*)A.coeff_v : (const uint8_t*)A.coeff_y2));
+			const u32x4* src = (const u32x4*)(isb ? A.bmode + m * 16 : base + idx * 32);
+			p.a = __builtin_nontemporal_load(src);
+			p.b = __builtin_nontemporal_load(isb ? src : src + 1);
+		} else {
+			p.a = u32x4{0u, 0u, 0u, 0u};
+			p.b = p.a;
 		}
+		const int q = ln & 3;  // lanes 26..29: ymode, uv_mode, segment_id, has_coeff
+		const uint8_t* sp = q == 2 ? A.ymode : (q == 3 ? A.uv_mode : (q == 0 ? A.segment_id : A.has_coeff));
+		p.side = sp[m];
 		return p;
 	};
 
@@ -458,10 +473,13 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			nxt = prefetch(lane, rA, two, (int)t + 1);
 
 			// per-half side info (lanes 26..29 / 58..61 hold it)
-			const int ymode = hh ? rdlane((int)cur.side, 58) : rdlane((int)cur.side, 26);
-			const int uvmode = hh ? rdlane((int)cur.side, 59) : rdlane((int)cur.side, 27);
-			const int seg = (hh ? rdlane((int)cur.side, 60) : rdlane((int)cur.side, 28)) & 3;
-			const int hasc = hh ? rdlane((int)cur.side, 61) : rdlane((int)cur.side, 29);
+			const int sd26 = rdlane((int)cur.side, 26), sd27 = rdlane((int)cur.side, 27), sd28 = rdlane((int)cur.side, 28),
+			          sd29 = rdlane((int)cur.side, 29), sd58 = rdlane((int)cur.side, 58), sd59 = rdlane((int)cur.side, 59),
+			          sd60 = rdlane((int)cur.side, 60), sd61 = rdlane((int)cur.side, 61);
+			const int ymode = hh ? sd58 : sd26;
+			const int uvmode = hh ? sd59 : sd27;
+			const int seg = (hh ? sd60 : sd28) & 3;
+			const int hasc = hh ? sd61 : sd29;
 			const bool bpred = ymode == 4;
 			const uint32_t y0 = r * 16, cy0 = r * 8, x0 = cu * 16, cx0 = cu * 8;
 
@@ -469,23 +487,22 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			// Computed before the dependency wait and parked in LDS (kResid, 32 B per block) so that
 			// no residual registers stay live across the wait.
 			if (!lf_only) {
-				int res[16];
+				// Packed int16 pairs: w[2r + h] = row r, columns 2h, 2h+1.  Dequantisation and the
+				// vertical pass wrap mod 2^16 exactly like the reference's int16 stores; the
+				// horizontal pass (whose (x + 4) >> 3 needs the full-precision sum) runs in 32 bits.
 				const int cls = ln < 16 ? 0 : (ln < 24 ? 1 : 2);  // Y1, UV, Y2 factors
-				const int16_t* dqt = (const int16_t*)(smem + kDqTable) + seg * 6 + cls * 2;
-				const int fdc = dqt[0], fac = dqt[1];
-				const uint32_t w8[8] = {cur.a.x, cur.a.y, cur.a.z, cur.a.w, cur.b.x, cur.b.y, cur.b.z, cur.b.w};
-				int v[16];
-				bool anyac = false;
-#pragma unroll
-				for (int i = 0; i < 16; i++) {
-					const int cf = (int)(int16_t)((w8[i >> 1] >> (16 * (i & 1))) & 0xFFFFu);
-					v[i] = sx16(cf * (i ? fac : fdc));
-					if (i) anyac |= v[i] != 0;
-				}
+				const uint32_t* dqt = (const uint32_t*)(smem + kDqTable) + seg * 3 + cls;
+				const uint32_t fdcac = *dqt;  // (dc, ac) int16 pair
+				const uint32_t facac = __builtin_amdgcn_perm(fdcac, fdcac, 0x03020302u);
+				uint32_t w[8] = {pk_mul(cur.a.x, fdcac), pk_mul(cur.a.y, facac), pk_mul(cur.a.z, facac), pk_mul(cur.a.w, facac),
+				                 pk_mul(cur.b.x, facac), pk_mul(cur.b.y, facac), pk_mul(cur.b.z, facac), pk_mul(cur.b.w, facac)};
+				const bool anyac = ((w[0] >> 16) | w[1] | w[2] | w[3] | w[4] | w[5] | w[6] | w[7]) != 0u;
 				// Y2 (non-B_PRED): inverse WHT (RFC 14.3) in the Y2 lane, 16 DCs to LDS
 				if (__ballot(act && !bpred) != 0ull) {
 					if (ln == 24 && act && !bpred) {
-						int t2[16], o[16];
+						int v[16], t2[16], o[16];
+#pragma unroll
+						for (int i = 0; i < 16; i++) v[i] = lo_s16(w[i >> 1] >> (16 * (i & 1)));
 #pragma unroll
 						for (int i = 0; i < 4; i++) {
 							const int a1 = v[i] + v[12 + i], b1 = v[4 + i] + v[8 + i];
@@ -499,51 +516,49 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 						for (int i = 0; i < 4; i++) {
 							const int* q = t2 + 4 * i;
 							const int a1 = q[0] + q[3], b1 = q[1] + q[2], c1 = q[1] - q[2], d1 = q[0] - q[3];
-							o[4 * i + 0] = sx16((a1 + b1 + 3) >> 3);
-							o[4 * i + 1] = sx16((c1 + d1 + 3) >> 3);
-							o[4 * i + 2] = sx16((a1 - b1 + 3) >> 3);
-							o[4 * i + 3] = sx16((d1 - c1 + 3) >> 3);
+							o[4 * i + 0] = (a1 + b1 + 3) >> 3;
+							o[4 * i + 1] = (c1 + d1 + 3) >> 3;
+							o[4 * i + 2] = (a1 - b1 + 3) >> 3;
+							o[4 * i + 3] = (d1 - c1 + 3) >> 3;
 						}
-						st128(hv + kWht, u32x4{lo16(o[0], o[1]), lo16(o[2], o[3]), lo16(o[4], o[5]), lo16(o[6], o[7])});
-						st128(hv + kWht + 16,
-						      u32x4{lo16(o[8], o[9]), lo16(o[10], o[11]), lo16(o[12], o[13]), lo16(o[14], o[15])});
+						st128(hv + kWht, u32x4{pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7])});
+						st128(hv + kWht + 16, u32x4{pack2(o[8], o[9]), pack2(o[10], o[11]), pack2(o[12], o[13]), pack2(o[14], o[15])});
 					}
 					wave_lds_sync();
-					if (ln < 16 && !bpred) v[0] = (int)*(const int16_t*)(hv + kWht + 2 * ln);
+					if (ln < 16 && !bpred) w[0] = (w[0] & 0xFFFF0000u) | *(const uint16_t*)(hv + kWht + 2 * ln);
 				}
 				// inverse DCT (RFC 14.4), whole 4x4 block per lane; DC-only shortcut when no lane
 				// of the wave has an AC coefficient ((dc+4)>>3 everywhere, exact)
+				uint32_t rs[8];
 				if (__ballot(anyac && ln < 24 && act) != 0ull) {
-					int t4[16];
+					uint32_t o[8];
 #pragma unroll
-					for (int i = 0; i < 4; i++) {
-						const int a1 = v[i] + v[8 + i], b1 = v[i] - v[8 + i];
-						const int c1 = mul_s(v[4 + i]) - mul_c(v[12 + i]), d1 = mul_c(v[4 + i]) + mul_s(v[12 + i]);
-						t4[i] = sx16(a1 + d1);
-						t4[12 + i] = sx16(a1 - d1);
-						t4[4 + i] = sx16(b1 + c1);
-						t4[8 + i] = sx16(b1 - c1);
+					for (int h = 0; h < 2; h++) {  // vertical pass, two columns per op
+						const uint32_t r0 = w[h], r1 = w[2 + h], r2 = w[4 + h], r3 = w[6 + h];
+						const uint32_t a1 = pk_add(r0, r2), b1 = pk_sub(r0, r2);
+						const uint32_t c1 = pk_sub(mul_s2(r1), mul_c2(r3)), d1 = pk_add(mul_c2(r1), mul_s2(r3));
+						o[h] = pk_add(a1, d1);
+						o[6 + h] = pk_sub(a1, d1);
+						o[2 + h] = pk_add(b1, c1);
+						o[4 + h] = pk_sub(b1, c1);
 					}
 #pragma unroll
-					for (int i = 0; i < 4; i++) {
-						const int* q = t4 + 4 * i;
-						const int a1 = q[0] + q[2], b1 = q[0] - q[2];
-						const int c1 = mul_s(q[1]) - mul_c(q[3]), d1 = mul_c(q[1]) + mul_s(q[3]);
-						res[4 * i + 0] = sx16((a1 + d1 + 4) >> 3);
-						res[4 * i + 3] = sx16((a1 - d1 + 4) >> 3);
-						res[4 * i + 1] = sx16((b1 + c1 + 4) >> 3);
-						res[4 * i + 2] = sx16((b1 - c1 + 4) >> 3);
+					for (int r = 0; r < 4; r++) {  // horizontal pass
+						const int x0 = lo_s16(o[2 * r]), x1 = hi_s16(o[2 * r]), x2 = lo_s16(o[2 * r + 1]), x3 = hi_s16(o[2 * r + 1]);
+						const int a1 = x0 + x2 + 4, b1 = x0 - x2 + 4;
+						const int c1 = mul_s(x1) - mul_c(x3), d1 = mul_c(x1) + mul_s(x3);
+						rs[2 * r] = pack2((a1 + d1) >> 3, (b1 + c1) >> 3);
+						rs[2 * r + 1] = pack2((b1 - c1) >> 3, (a1 - d1) >> 3);
 					}
 				} else {
-					const int d = (v[0] + 4) >> 3;
+					const int d = (lo_s16(w[0]) + 4) >> 3;
 #pragma unroll
-					for (int i = 0; i < 16; i++) res[i] = d;
+					for (int i = 0; i < 8; i++) rs[i] = pack2(d, d);
 				}
 				if (ln < 24) {
 					uint8_t* rp = hv + kResid + ln * 32;
-					st128(rp, u32x4{lo16(res[0], res[1]), lo16(res[2], res[3]), lo16(res[4], res[5]), lo16(res[6], res[7])});
-					st128(rp + 16,
-					      u32x4{lo16(res[8], res[9]), lo16(res[10], res[11]), lo16(res[12], res[13]), lo16(res[14], res[15])});
+					st128(rp, u32x4{rs[0], rs[1], rs[2], rs[3]});
+					st128(rp + 16, u32x4{rs[4], rs[5], rs[6], rs[7]});
 				}
 			}
 			STAMP(0);
