@@ -41,8 +41,20 @@ $(BIN)/decoder: $(PKG)/host/decoder_main.c $(LIB)/libvp8host.so $(LIB)/libvp8g.s
 oracle:
 	$(MAKE) -C oracle
 
+# Diagnostic variants of libvp8g (never loaded by the product path; select with VP8G_LIB=...):
+# per-phase shader-clock stamps, and phase ablations (timing only, wrong output).
+DIAG := $(LIB)/diag
+DIAG_VARIANTS := stamps abl1 abl2 abl4 abl8 abl15
+diag: $(foreach v,$(DIAG_VARIANTS),$(DIAG)/libvp8g_$(v).so)
+$(DIAG):
+	mkdir -p $@
+$(DIAG)/libvp8g_stamps.so: $(HIP_SRC) $(HIP_HDR) | $(DIAG)
+	$(HIPCC) $(HIPFLAGS) -DVP8G_STAMPS -shared -Wl,-Bsymbolic -o $@ $(HIP_SRC) -lpthread
+$(DIAG)/libvp8g_abl%.so: $(HIP_SRC) $(HIP_HDR) | $(DIAG)
+	$(HIPCC) $(HIPFLAGS) -DVP8G_ABLATE=$* -shared -Wl,-Bsymbolic -o $@ $(HIP_SRC) -lpthread
+
 clean:
 	rm -rf $(LIB) $(BIN)
 	$(MAKE) -C oracle clean
 
-.PHONY: all lib oracle clean
+.PHONY: all lib oracle clean diag

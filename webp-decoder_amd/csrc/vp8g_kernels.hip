@@ -64,6 +64,7 @@ namespace {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) u32x4 gu32x4;  // global-memory vector (never flat)
 
 // ---------------------------------------------------------------------------------------------
 // B_PRED predictor table (RFC 6386 12.3; reference vp8_recon.c:218-358).  A lane predicting one
@@ -209,6 +210,14 @@ DEV uint32_t mulhi2(uint32_t x, int c) {
 }
 DEV uint32_t mul_s2(uint32_t x) { return pk_add(x, mulhi2(x, 35468 - 65536)); }  // mul_s of both halves, mod 2^16
 DEV uint32_t mul_c2(uint32_t x) { return pk_add(x, mulhi2(x, 20091)); }
+// c ? a : b per lane, as two v_cndmask (opaque to the optimiser)
+DEV uint64_t vsel(bool c, uint64_t a, uint64_t b) {
+	const uint64_t mk = __builtin_amdgcn_ballot_w64(c);
+	uint32_t lo, hi;
+	asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(lo) : "v"((uint32_t)b), "v"((uint32_t)a), "s"(mk));
+	asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(hi) : "v"((uint32_t)(b >> 32)), "v"((uint32_t)(a >> 32)), "s"(mk));
+	return ((uint64_t)hi << 32) | lo;
+}
 DEV int rdlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 
 // Per-frame context (unfiltered bottom rows + filter-state bottom rows per MB column), in LDS
@@ -426,21 +435,26 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 		const int cn = tt - 2 * hh;
 		const bool inb = (hh == 0 || two) && cn >= 0 && cn < (int)C;
 		const uint64_t m = mb0 + (inb ? (uint64_t)((rA + hh) * C + (uint32_t)cn) : 0ull);
-		if (!lf_only) {
+		// Issued unconditionally (loop-filter-only frames read the descriptor instead of the
+		// absent coefficient arrays): a path without these loads would make the compiler's
+		// wait-count analysis fall back to vmcnt(0) on the next step's use of the side bytes,
+		// i.e. wait for this very prefetch.
+		{
 			const bool isb = ln == 25;
 			const uint64_t idx = ln < 16 ? m * 16 + ln : (ln < 24 ? m * 4 + (ln & 3) : m);
-			const uint8_t* base = ln < 16 ? (const uint8_t*)A.coeff_y
-			                              : (ln < 20 ? (const uint8_t*)A.coeff_u : (ln < 24 ? (const uint8_t*)A.coeff_v : (const uint8_t*)A.coeff_y2));
-			const u32x4* src = (const u32x4*)(isb ? A.bmode + m * 16 : base + idx * 32);
+			// (vsel: explicit v_cndmask -- a select among struct fields by a lane-dependent index
+			// would otherwise compile to a per-lane load from the kernel-argument block)
+			const uint64_t base = vsel(ln < 16, (uint64_t)A.coeff_y,
+			                           vsel(ln < 20, (uint64_t)A.coeff_u, vsel(ln < 24, (uint64_t)A.coeff_v, (uint64_t)A.coeff_y2)));
+			const uint64_t addr = vsel(isb, (uint64_t)A.bmode + m * 16, base + idx * 32);
+			const gu32x4* src = (const gu32x4*)(lf_only ? (uint64_t)descs : addr);
 			p.a = __builtin_nontemporal_load(src);
 			p.b = __builtin_nontemporal_load(isb ? src : src + 1);
-		} else {
-			p.a = u32x4{0u, 0u, 0u, 0u};
-			p.b = p.a;
 		}
 		const int q = ln & 3;  // lanes 26..29: ymode, uv_mode, segment_id, has_coeff
-		const uint8_t* sp = q == 2 ? A.ymode : (q == 3 ? A.uv_mode : (q == 0 ? A.segment_id : A.has_coeff));
-		p.side = sp[m];
+		const uint8_t* sp = (const uint8_t*)vsel(q == 2, (uint64_t)A.ymode,
+		                                         vsel(q == 3, (uint64_t)A.uv_mode, vsel(q == 0, (uint64_t)A.segment_id, (uint64_t)A.has_coeff)));
+		p.side = ((const __attribute__((address_space(1))) uint8_t*)sp)[m];
 		return p;
 	};
 
