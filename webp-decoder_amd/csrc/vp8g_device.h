@@ -11,8 +11,8 @@ namespace vp8g {
 // half; each half owns one of these areas.  16-B aligned where a 16-B access is made.
 constexpr int kLfY = 0;       // luma filter tile: 20 rows x 32 cols (4 rows above + 16 MB rows;
                               // two MB columns as a ring, slot = mb_col & 1)
-constexpr int kLfU = 640;     // chroma tiles: 12 rows x 16 cols (4 above + 8 MB rows; ring of 2)
-constexpr int kLfV = 832;
+constexpr int kLfUV = 640;    // chroma tile: 12 rows x 32 B (4 above + 8 MB rows); per row U at +0,
+                              // V at +16, each a ring of two 8-B MB columns (slot = mb_col & 1)
 constexpr int kAbY = 1024;    // luma above row: [15] corner P, [16..31] A, [32..35] above-right
 constexpr int kAbUV = 1072;   // chroma above rows: U P@7 A@8..15, V P@23 A@24..31
 constexpr int kColY = 1104;   // B_PRED: luma columns 11, 7, 3 of the MB (16 B each, in that order),

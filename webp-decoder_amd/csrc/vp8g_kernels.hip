@@ -218,6 +218,9 @@ DEV uint64_t vsel(bool c, uint64_t a, uint64_t b) {
 	asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(hi) : "v"((uint32_t)(b >> 32)), "v"((uint32_t)(a >> 32)), "s"(mk));
 	return ((uint64_t)hi << 32) | lo;
 }
+// single-byte LDS access that the load/store vectoriser leaves alone
+DEV int ldb(const uint8_t* p) { return (int)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT); }
+DEV void stb(uint8_t* p, int v) { __hip_atomic_store(p, (uint8_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT); }
 DEV int rdlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 
 // Per-frame context (unfiltered bottom rows + filter-state bottom rows per MB column), in LDS
@@ -255,118 +258,123 @@ DEV uint32_t lf_off(uint32_t c) { return c * kCtxBytesPerCol + kCtxRecBytes; }
 
 // ---------------------------------------------------------------------------------------------
 // Loop filter on a line of pixels (RFC 6386 15.2-15.4; reference vp8_loopfilter.c:24-164),
-// branch-free.  A line is 20 pixels held as 5 packed dwords: w[0] = the neighbour's last 4
-// pixels (left or above), w[1..4] = this MB; the edge at dword j has p3 p2 p1 p0 = bytes 0..3 of
-// w[j-1] and q0 q1 q2 q3 = bytes 0..3 of w[j] (j = 1: MB edge, 2..4: sub-block edges).
+// branch-free, on unpacked bytes: a line is px[0..19] = the neighbour's last 4 pixels (left or
+// above) and this MB's 16 (chroma: 8); the edge at 4j (j = 1 MB edge, 2..4 sub-block edges) has
+// p3..p0 = px[4j-4..4j-1], q0..q3 = px[4j..4j+3].  Lines are gathered / scattered with LDS byte
+// loads and stores at immediate offsets, so no vector instruction is spent on (un)packing.
 // ---------------------------------------------------------------------------------------------
-struct EdgePx {
-	int p3, p2, p1, p0, q0, q1, q2, q3;
-};
-DEV EdgePx unpack_edge(uint32_t wp, uint32_t wq) {
-	return EdgePx{ubyte(wp, 0), ubyte(wp, 1), ubyte(wp, 2), ubyte(wp, 3), ubyte(wq, 0), ubyte(wq, 1), ubyte(wq, 2), ubyte(wq, 3)};
-}
 // normal-filter edge mask (RFC 15.3 filter_yes + interior limits) and high-edge-variance
-DEV void edge_mask(const EdgePx& e, bool en, int lim, int I, int T, bool& m, bool& hev) {
-	const int d10 = ad(e.p1, e.p0), e10 = ad(e.q1, e.q0);
-	const int interior = max(max3i(ad(e.p3, e.p2), ad(e.p2, e.p1), d10), max3i(ad(e.q3, e.q2), ad(e.q2, e.q1), e10));
-	m = en && (ad(e.p0, e.q0) * 2 + (ad(e.p1, e.q1) >> 1) <= lim) && interior <= I;
+DEV void edge_mask(const int* x, bool en, int lim, int I, int T, bool& m, bool& hev) {
+	const int d10 = ad(x[2], x[3]), e10 = ad(x[5], x[4]);
+	const int interior = max(max3i(ad(x[0], x[1]), ad(x[1], x[2]), d10), max3i(ad(x[7], x[6]), ad(x[6], x[5]), e10));
+	const bool fy = ad(x[3], x[4]) * 2 + (ad(x[2], x[5]) >> 1) <= lim;
+	m = en & fy & (interior <= I);
 	hev = max(d10, e10) > T;
 }
 
-DEV void lf_mb_edge(uint32_t& wp, uint32_t& wq, bool en, int lim, int I, int T) {  // normal, MB edge
-	const EdgePx e = unpack_edge(wp, wq);
+DEV void lf_mb_edge(int* x, bool en, int lim, int I, int T) {  // normal, MB edge
 	bool m, hev;
-	edge_mask(e, en, lim, I, T, m, hev);
-	const int w = sclamp(sclamp(e.p1 - e.q1) + 3 * (e.q0 - e.p0));
+	edge_mask(x, en, lim, I, T, m, hev);
+	const int p2 = x[1], p1 = x[2], p0 = x[3], q0 = x[4], q1 = x[5], q2 = x[6];
+	const int w = sclamp(sclamp(p1 - q1) + 3 * (q0 - p0));
 	const int f1 = sclamp(w + 4) >> 3, f2 = sclamp(w + 3) >> 3;
 	const int a27 = (27 * w + 63) >> 7, a18 = (18 * w + 63) >> 7, a9 = (9 * w + 63) >> 7;
-	const bool mh = m && hev, mn = m && !hev;
-	const int np0 = mh ? sat8(e.p0 + f2) : (mn ? sat8(e.p0 + a27) : e.p0);
-	const int nq0 = mh ? sat8(e.q0 - f1) : (mn ? sat8(e.q0 - a27) : e.q0);
-	const int np1 = mn ? sat8(e.p1 + a18) : e.p1, nq1 = mn ? sat8(e.q1 - a18) : e.q1;
-	const int np2 = mn ? sat8(e.p2 + a9) : e.p2, nq2 = mn ? sat8(e.q2 - a9) : e.q2;
-	wp = pack4(e.p3, np2, np1, np0);
-	wq = pack4(nq0, nq1, nq2, e.q3);
+	const bool mh = m & hev, mn = m & !hev;
+	const int d0p = mh ? f2 : a27, d0q = mh ? f1 : a27;
+	x[3] = m ? sat8(p0 + d0p) : p0;
+	x[4] = m ? sat8(q0 - d0q) : q0;
+	x[2] = mn ? sat8(p1 + a18) : p1;
+	x[5] = mn ? sat8(q1 - a18) : q1;
+	x[1] = mn ? sat8(p2 + a9) : p2;
+	x[6] = mn ? sat8(q2 - a9) : q2;
 }
 
-DEV void lf_sub_edge(uint32_t& wp, uint32_t& wq, bool en, int lim, int I, int T) {  // normal, sub-block edge
-	const EdgePx e = unpack_edge(wp, wq);
+DEV void lf_sub_edge(int* x, bool en, int lim, int I, int T) {  // normal, sub-block edge
 	bool m, hev;
-	edge_mask(e, en, lim, I, T, m, hev);
-	const int a = sclamp(3 * (e.q0 - e.p0) + (hev ? sclamp(e.p1 - e.q1) : 0));
+	edge_mask(x, en, lim, I, T, m, hev);
+	const int p1 = x[2], p0 = x[3], q0 = x[4], q1 = x[5];
+	const int a = sclamp(3 * (q0 - p0) + (hev ? sclamp(p1 - q1) : 0));
 	const int f1 = sclamp(a + 4) >> 3, f2 = sclamp(a + 3) >> 3;
 	const int a2 = (f1 + 1) >> 1;
-	const bool mn = m && !hev;
-	const int nq0 = m ? sat8(e.q0 - f1) : e.q0, np0 = m ? sat8(e.p0 + f2) : e.p0;
-	const int nq1 = mn ? sat8(e.q1 - a2) : e.q1, np1 = mn ? sat8(e.p1 + a2) : e.p1;
-	wp = pack4(e.p3, e.p2, np1, np0);
-	wq = pack4(nq0, nq1, e.q2, e.q3);
+	const bool mn = m & !hev;
+	x[4] = m ? sat8(q0 - f1) : q0;
+	x[3] = m ? sat8(p0 + f2) : p0;
+	x[5] = mn ? sat8(q1 - a2) : q1;
+	x[2] = mn ? sat8(p1 + a2) : p1;
 }
 
-DEV void lf_simple_edge(uint32_t& wp, uint32_t& wq, bool en, int lim) {  // simple filter (luma only)
-	const int p1 = ubyte(wp, 2), p0 = ubyte(wp, 3), q0 = ubyte(wq, 0), q1 = ubyte(wq, 1);
-	const bool m = en && ad(p0, q0) * 2 + (ad(p1, q1) >> 1) <= lim;
+DEV void lf_simple_edge(int* x, bool en, int lim) {  // simple filter (luma only)
+	const int p1 = x[2], p0 = x[3], q0 = x[4], q1 = x[5];
+	const bool m = en & (ad(p0, q0) * 2 + (ad(p1, q1) >> 1) <= lim);
 	const int a = sclamp(sclamp(p1 - q1) + 3 * (q0 - p0));
-	const int nq0 = m ? sat8(q0 - (sclamp(a + 4) >> 3)) : q0, np0 = m ? sat8(p0 + (sclamp(a + 3) >> 3)) : p0;
-	wp = (wp & 0x0000FFFFu) | ((uint32_t)p1 << 16) | ((uint32_t)np0 << 24);
-	wq = (wq & 0xFFFF0000u) | (uint32_t)nq0 | ((uint32_t)q1 << 8);
+	x[4] = m ? sat8(q0 - (sclamp(a + 4) >> 3)) : q0;
+	x[3] = m ? sat8(p0 + (sclamp(a + 3) >> 3)) : p0;
 }
 
 // All edges of one line, in the reference order (MB edge, then sub-block edges).  `is_y`
-// enables the luma-only edges at dwords 3 and 4; chroma has its single inner edge at dword 2.
+// enables the luma-only edges at 12 and 16; chroma has its single inner edge at 8.
 template <bool kSimple>
-DEV void lf_line(uint32_t* w, bool mb_edge, bool inner, bool is_y, int E, int I, int T) {
+DEV void lf_line(int* px, bool mb_edge, bool inner, bool is_y, int E, int I, int T) {
 	if constexpr (kSimple) {
-		lf_simple_edge(w[0], w[1], mb_edge && is_y, (E + 2) * 2 + I);
-		lf_simple_edge(w[1], w[2], inner && is_y, E * 2 + I);
-		lf_simple_edge(w[2], w[3], inner && is_y, E * 2 + I);
-		lf_simple_edge(w[3], w[4], inner && is_y, E * 2 + I);
+		lf_simple_edge(px + 0, mb_edge & is_y, (E + 2) * 2 + I);
+		lf_simple_edge(px + 4, inner & is_y, E * 2 + I);
+		lf_simple_edge(px + 8, inner & is_y, E * 2 + I);
+		lf_simple_edge(px + 12, inner & is_y, E * 2 + I);
 	} else {
-		lf_mb_edge(w[0], w[1], mb_edge, 2 * (E + 2) + I, I, T);
-		lf_sub_edge(w[1], w[2], inner, 2 * E + I, I, T);
-		lf_sub_edge(w[2], w[3], inner && is_y, 2 * E + I, I, T);
-		lf_sub_edge(w[3], w[4], inner && is_y, 2 * E + I, I, T);
+		lf_mb_edge(px + 0, mb_edge, 2 * (E + 2) + I, I, T);
+		lf_sub_edge(px + 4, inner, 2 * E + I, I, T);
+		lf_sub_edge(px + 8, inner & is_y, 2 * E + I, I, T);
+		lf_sub_edge(px + 12, inner & is_y, 2 * E + I, I, T);
 	}
 }
 
-// Both passes of the loop filter over this lane's line of the MB held in LDS.
+// Both passes of the loop filter over this lane's line of the MB held in LDS.  Lanes 0..15:
+// luma rows / columns; 16..23 U, 24..31 V.  Bytes that may change: 1..17 (luma), 1..9 (chroma).
 template <bool kSimple>
-DEV void lf_mb(uint8_t* tY, uint8_t* tU, uint8_t* tV, int ln, int slot, bool en, bool mb_v, bool mb_h, bool inner, int E,
-               int I, int T) {
+DEV void lf_mb(uint8_t* tY, uint8_t* tC, int ln, int slot, bool en, bool mb_v, bool mb_h, bool inner, int E, int I, int T) {
 	const bool isy = ln < 16;
-	// vertical edges: one line per lane along a pixel row (Y 16, U 8, V 8)
+	const int cp = (ln >> 3) & 1;
+	const bool wr = en && (isy || !kSimple);
+	int px[20];
+	// vertical edges: one line per lane along a pixel row; the neighbour's 4 pixels sit at the
+	// other end of the 2-MB ring when slot == 0
 	{
-		uint8_t* rowp = isy ? tY + (4 + ln) * 32 : (ln < 24 ? tU : tV) + (4 + (ln & 7)) * 16;
-		const int ring = isy ? 7 : 3;  // dword ring of the two-MB tile row
-		const int base = isy ? slot * 4 : slot * 2;
-		uint32_t w[5];
+		// (ldb/stb: relaxed wave-scope atomics keep the byte accesses single ds_read_u8 /
+		// ds_write_b8 -- merged wide accesses cost vector instructions to (un)pack)
+		uint8_t* const rowp = isy ? tY + (4 + ln) * 32 : tC + (4 + (ln & 7)) * 32 + cp * 16;
+		const int off = isy ? slot * 16 : slot * 8, ring = isy ? 31 : 15;
+		uint8_t* const Lp = rowp + ((off - 4) & ring);
+		uint8_t* const Mp = rowp + off;
 #pragma unroll
-		for (int q = 0; q < 5; q++) w[q] = (q < 3 || isy) ? ld32(rowp + 4 * ((base - 1 + q) & ring)) : 0u;
-		lf_line<kSimple>(w, en && mb_v, en && inner, isy, E, I, T);
-		if (en && (isy || !kSimple)) {
+		for (int i = 0; i < 4; i++) px[i] = ldb(Lp + i);
 #pragma unroll
-			for (int q = 0; q < 5; q++)
-				if (q < 3 || isy) st32(rowp + 4 * ((base - 1 + q) & ring), w[q]);
+		for (int i = 0; i < 16; i++) px[4 + i] = ldb(Mp + i);
+		lf_line<kSimple>(px, en && mb_v, en && inner, isy, E, I, T);
+		if (wr) {
+#pragma unroll
+			for (int i = 1; i < 4; i++) stb(Lp + i, px[i]);
+#pragma unroll
+			for (int i = 0; i < 6; i++) stb(Mp + i, px[4 + i]);
+			if (isy) {
+#pragma unroll
+				for (int i = 6; i < 14; i++) stb(Mp + i, px[4 + i]);
+			}
 		}
 	}
 	wave_lds_sync();
-	// horizontal edges: one line per lane down a pixel column
+	// horizontal edges: one line per lane down a pixel column (tile rows 0..19, pitch 32)
 	{
-		uint8_t* colp = isy ? tY + slot * 16 + ln : (ln < 24 ? tU : tV) + slot * 8 + (ln & 7);
-		const int stride = isy ? 32 : 16;
-		uint32_t w[5];
+		uint8_t* const colp = isy ? tY + slot * 16 + ln : tC + cp * 16 + slot * 8 + (ln & 7);
 #pragma unroll
-		for (int q = 0; q < 5; q++) {
-			if (q < 3 || isy)
-				w[q] = pack4(colp[(4 * q) * stride], colp[(4 * q + 1) * stride], colp[(4 * q + 2) * stride],
-				             colp[(4 * q + 3) * stride]);
-			else w[q] = 0u;
-		}
-		lf_line<kSimple>(w, en && mb_h, en && inner, isy, E, I, T);
-		if (en && (isy || !kSimple)) {
+		for (int i = 0; i < 20; i++) px[i] = ldb(colp + 32 * i);
+		lf_line<kSimple>(px, en && mb_h, en && inner, isy, E, I, T);
+		if (wr) {
 #pragma unroll
-			for (int q = 1; q < 19; q++)
-				if (q < 11 || isy) colp[q * stride] = (uint8_t)ubyte(w[q >> 2], q & 3);
+			for (int i = 1; i < 10; i++) stb(colp + 32 * i, px[i]);
+			if (isy) {
+#pragma unroll
+				for (int i = 10; i < 18; i++) stb(colp + 32 * i, px[i]);
+			}
 		}
 	}
 	wave_lds_sync();
@@ -477,8 +485,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			const int slot = c & 1;
 			uint8_t* const hv = smem + kHdrBytes + wave * kWaveBytes + hh * kHalfBytes;  // this half's area
 			uint8_t* const tY = hv + kLfY;
-			uint8_t* const tU = hv + kLfU;
-			uint8_t* const tV = hv + kLfV;
+			uint8_t* const tC = hv + kLfUV;  // chroma: U at +0, V at +16, row pitch 32
 			uint8_t* const abY = hv + kAbY;
 			uint8_t* const abUV = hv + kAbUV;
 			uint8_t* const left = hv + kLeft;
@@ -610,7 +617,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					} else {
 						const int p = (ln - 16) >> 3, row = ln & 7;
 						const uint8_t* s = src + (p ? D.src_v : D.src_u) + (size_t)(cy0 + row) * D.src_stride_uv + cx0;
-						st64((p ? tV : tU) + (4 + row) * 16 + slot * 8, u32x2{ld32(s), ld32(s + 4)});
+						st64(tC + p * 16 + (4 + row) * 32 + slot * 8, u32x2{ld32(s), ld32(s + 4)});
 					}
 				} else {
 					// ln 0..3 luma above row, 4 luma above-right (cols x+16..x+19, clamped to the
@@ -635,7 +642,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					const bool ly = ln < 24;
 					const int p = (ln - 24) >> 2, tr = ly ? ln - 20 : (ln - 24) & 3;
 					const uint32_t lo = lf_off(cu) + (ly ? tr * 16 : 64 + p * 32 + tr * 8);
-					uint8_t* const td = ly ? tY + tr * 32 + slot * 16 : (p ? tV : tU) + tr * 16 + slot * 8;
+					uint8_t* const td = ly ? tY + tr * 32 + slot * 16 : tC + p * 16 + tr * 32 + slot * 8;
 					st64(td, ctx.rd64(lo));
 					if (ly) st64(td + 8, ctx.rd64(lo + 8));
 				}
@@ -672,8 +679,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					const uint32_t mL = (mode == 2 || mode == 3) ? 0xFFu : 0u;
 					const int K = (mode == 3 ? -P : 0) + (mode == 0 ? dcv : 0);
 					uint8_t* dst = yl ? tY + (4 + 4 * by) * 32 + slot * 16 + 4 * bx
-					                  : (p ? tV : tU) + (4 + 4 * by) * 16 + slot * 8 + 4 * bx;
-					const int dstride = yl ? 32 : 16;
+					                  : tC + p * 16 + (4 + 4 * by) * 32 + slot * 8 + 4 * bx;
 					const u32x4 r01 = ld128(hv + kResid + ln * 32), r23 = ld128(hv + kResid + ln * 32 + 16);
 					const uint32_t rw[8] = {r01.x, r01.y, r01.z, r01.w, r23.x, r23.y, r23.z, r23.w};
 					int acol[4];
@@ -688,7 +694,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 							const int rv = (int)(int16_t)((rw[(4 * rr + cc) >> 1] >> (16 * (cc & 1))) & 0xFFFFu);
 							px4[cc] = sat8(sat8(L + acol[cc]) + rv);
 						}
-						st32(dst + rr * dstride, pack4(px4[0], px4[1], px4[2], px4[3]));
+						st32(dst + rr * 32, pack4(px4[0], px4[1], px4[2], px4[3]));
 					}
 				}
 				wave_lds_sync();
@@ -763,11 +769,11 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			if (act && !lf_only) {
 				// right column -> left column of the next MB (Y 16, U 8, V 8 lanes)
 				const uint8_t* sp = ln < 16 ? tY + (4 + ln) * 32 + slot * 16 + 15
-				                            : (ln < 24 ? tU : tV) + (4 + (ln & 7)) * 16 + slot * 8 + 7;
+				                            : tC + ((ln >> 3) & 1) * 16 + (4 + (ln & 7)) * 32 + slot * 8 + 7;
 				const uint8_t pxv = *sp;
 				if (ln == 0) ctx.wr128(rec_off(cu), ld128(tY + 19 * 32 + slot * 16));  // bottom rows -> ctx_rec[c]
-				else if (ln == 1) ctx.wr64(rec_off(cu) + 16, ld64(tU + 11 * 16 + slot * 8));
-				else if (ln == 2) ctx.wr64(rec_off(cu) + 24, ld64(tV + 11 * 16 + slot * 8));
+				else if (ln == 1) ctx.wr64(rec_off(cu) + 16, ld64(tC + 11 * 32 + slot * 8));
+				else if (ln == 2) ctx.wr64(rec_off(cu) + 24, ld64(tC + 16 + 11 * 32 + slot * 8));
 				else if (ln == 3) {  // corner for the next MB
 					abY[15] = abY[31];
 					abUV[7] = abUV[15];
@@ -785,8 +791,8 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 				const bool en = act && E != 0;
 				if (__ballot(en) != 0ull) {
 					const bool inner = hasc != 0 || bpred;
-					if (simple) lf_mb<true>(tY, tU, tV, ln, slot, en, c > 0, r > 0, inner, E, I, Tt);
-					else lf_mb<false>(tY, tU, tV, ln, slot, en, c > 0, r > 0, inner, E, I, Tt);
+					if (simple) lf_mb<true>(tY, tC, ln, slot, en, c > 0, r > 0, inner, E, I, Tt);
+					else lf_mb<false>(tY, tC, ln, slot, en, c > 0, r > 0, inner, E, I, Tt);
 				}
 			}
 			STAMP(5);
@@ -818,7 +824,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			if (!lf_on) {
 				// unfiltered: MB(r, c) is final as soon as it is reconstructed
 				const int pl = ln < 16 ? 0 : ((ln - 16) >> 3) + 1, row = ln < 16 ? ln : (ln & 7);
-				const uint8_t* src = ln < 16 ? tY + (4 + ln) * 32 + slot * 16 : (pl == 2 ? tV : tU) + (4 + row) * 16 + slot * 8;
+				const uint8_t* src = ln < 16 ? tY + (4 + ln) * 32 + slot * 16 : tC + (pl - 1) * 16 + (4 + row) * 32 + slot * 8;
 				emit(act, pl, (ln < 16 ? y0 : cy0) + row, cu, src);
 			} else {
 				const bool last_row = r + 1 == R;
@@ -834,7 +840,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					const int sl = slot ^ prev;
 					// tile row: top strip 0..3, body 4.., tail 16.. (luma) / 8.. (chroma); image row = base + trow - 4
 					const int trow = kind == 0 ? kk : (kind == 1 ? 4 + kk : (isy ? 16 : 8) + kk);
-					const uint8_t* src = isy ? tY + trow * 32 + sl * 16 : (pl == 2 ? tV : tU) + trow * 16 + sl * 8;
+					const uint8_t* src = isy ? tY + trow * 32 + sl * 16 : tC + (pl - 1) * 16 + trow * 32 + sl * 8;
 					const bool to_ctx = ok && kind == 2 && !last_row;
 					if (to_ctx) {
 						const uint32_t off = lf_off(col) + (isy ? kk * 16 : 64 + (pl - 1) * 32 + kk * 8);
