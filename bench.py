@@ -42,6 +42,7 @@ import torch
 ROOT = pathlib.Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "webp-decoder_amd"))
 import vp8g  # noqa: E402
+import vp8g_dist  # noqa: E402
 
 FIXTURES = [
     "big/uhd_a_normal_seg4.webp",
@@ -150,9 +151,8 @@ def main():
     frames = [vp8g.decode_file(ROOT / "tests" / "fixtures" / r) for r in FIXTURES]
     W, H = frames[0].width, frames[0].height
     batch = Batch(frames, args.frames, filtered, dev)
-    if dist is not None:
-        # per-frame parameter blocks (dequant + loop-filter tables) are shared: rank 0's go to all
-        dist.broadcast(batch.d_descs, src=0)
+    # per-frame parameter blocks (dequant + loop-filter tables) are shared: rank 0's go to all
+    vp8g_dist.share_frame_params(batch.d_descs, dist)
     stream = torch.cuda.current_stream(dev)
 
     for _ in range(args.warmup):
@@ -180,17 +180,15 @@ def main():
     if int(batch.status[0].item()) != 0:
         raise RuntimeError("kernel reported a dependency-wait timeout")
 
-    # parity spot check: 4 slots (one per fixture) vs the reference decoder's hashes
+    # parity spot check: 4 slots (one per fixture) vs the reference decoder's hashes; the
+    # per-frame digests of all ranks are gathered (64 bits each, never pixels)
     key = "yuvf_sha256" if filtered else "yuv_sha256"
-    ok = all(hashlib.sha256(batch.frame_output(i, W, H)).hexdigest() == manifest["files"][FIXTURES[i % 4]][key]
-             for i in range(min(4, args.frames)))
-    if dist is not None:
-        t = torch.tensor([elapsed, kern_ms, float(ok)], dtype=torch.float64, device=dev)
-        tmax = t.clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        tmin = t.clone()
-        dist.all_reduce(tmin, op=dist.ReduceOp.MIN)
-        elapsed, kern_ms, ok = float(tmax[0]), float(tmax[1]), bool(tmin[2] > 0.5)
+    outs = [batch.frame_output(i, W, H) for i in range(min(4, args.frames))]
+    ok = all(hashlib.sha256(o).hexdigest() == manifest["files"][FIXTURES[i % 4]][key] for i, o in enumerate(outs))
+    digests = torch.tensor([vp8g_dist.digest64(o) for o in outs], dtype=torch.int64, device=dev)
+    all_digests = vp8g_dist.gather_frame_digests(digests, dist)
+    ok = ok and bool((all_digests == all_digests[0]).all())  # every rank decoded the same fixtures alike
+    elapsed, kern_ms, ok = vp8g_dist.reduce_timing(elapsed, kern_ms, ok, dist, dev)
 
     total_frames = args.frames * world
     mp = total_frames * W * H / 1e6

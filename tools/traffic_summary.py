@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""Turn a tools/profile_round.sh run into the committed profile files.
+
+  tools/traffic_summary.py <tag>   (reads gpurun_out/prof_<tag>/, writes profiles/)
+
+* profiles/<tag>_kernel_stats.csv   -- rocprofv3 --stats summary of the bench command
+* profiles/<tag>_trace_bench.json   -- the bench line printed under the profiler
+* profiles/traffic_4k_batch.json    -- HBM bytes per launch of the bench kernel from the PMC
+  passes: FETCH_SIZE (KiB; x2 on gfx950 for wide coalesced reads, MI355X_MICROARCH.md "HBM")
+  + WRITE_SIZE (KiB), averaged over the frame_kernel dispatches.  bench.py reports it as
+  roofline.traffic.
+"""
+import csv
+import glob
+import json
+import os
+import pathlib
+import shutil
+import sys
+
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+tag = sys.argv[1]
+src = ROOT / "gpurun_out" / f"prof_{tag}"
+prof = ROOT / "profiles"
+prof.mkdir(exist_ok=True)
+
+stats = glob.glob(str(src / "trace" / "**" / "*kernel_stats.csv"), recursive=True)
+if stats:
+    shutil.copy(stats[0], prof / f"{tag}_kernel_stats.csv")
+bench_line = None
+for line in open(src / "trace_bench.log"):
+    if line.startswith("{"):
+        bench_line = json.loads(line)
+if bench_line:
+    (prof / f"{tag}_trace_bench.json").write_text(json.dumps(bench_line, indent=1) + "\n")
+
+
+def per_dispatch(counter):
+    f = glob.glob(str(src / f"pmc_{counter}" / "**" / "*counter_collection.csv"), recursive=True)[0]
+    tot, disp = 0.0, set()
+    for r in csv.DictReader(open(f)):
+        if "frame_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            tot += float(r["Counter_Value"])
+            disp.add(r["Dispatch_Id"])
+    return tot / len(disp), len(disp)
+
+
+fetch_kib, n1 = per_dispatch("FETCH_SIZE")
+write_kib, n2 = per_dispatch("WRITE_SIZE")
+read_b = fetch_kib * 1024 * 2
+write_b = write_kib * 1024
+mbs = 512 * 240 * 135
+out = {
+    "frames": 512, "filtered": True, "width": 3840, "height": 2160,
+    "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, {n1}/{n2} dispatches of frame_kernel<8,false>, tag {tag}",
+    "fetch_size_kib_per_launch": round(fetch_kib, 1),
+    "write_size_kib_per_launch": round(write_kib, 1),
+    "hbm_read_bytes_per_launch": round(read_b),
+    "hbm_write_bytes_per_launch": round(write_b),
+    "hbm_bytes_per_launch": round(read_b + write_b),
+    "per_mb": {"read": round(read_b / mbs, 1), "write": round(write_b / mbs, 1),
+               "algorithmic_read": 820, "algorithmic_write": 384},
+    "note": "FETCH_SIZE doubled (gfx950 tallies 128-B requests at 64 B); write amplification = "
+            "partial-line row pieces (16 B luma / 8 B chroma per row per MB) evicted before "
+            "their neighbours arrive",
+}
+(prof / "traffic_4k_batch.json").write_text(json.dumps(out, indent=1) + "\n")
+print(json.dumps(out, indent=1))
