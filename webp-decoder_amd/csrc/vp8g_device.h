@@ -9,18 +9,20 @@ namespace vp8g {
 
 // Per-half-wave LDS scratch (bytes).  A wave works on two macroblocks at once, one per 32-lane
 // half; each half owns one of these areas.  16-B aligned where a 16-B access is made.
-constexpr int kLfY = 0;       // luma filter tile: 20 rows x 32 cols (4 rows above + 16 MB rows;
-                              // two MB columns as a ring, slot = mb_col & 1)
-constexpr int kLfUV = 640;    // chroma tile: 12 rows x 32 B (4 above + 8 MB rows); per row U at +0,
-                              // V at +16, each a ring of two 8-B MB columns (slot = mb_col & 1)
-constexpr int kAbY = 1024;    // luma above row: [15] corner P, [16..31] A, [32..35] above-right
-constexpr int kAbUV = 1072;   // chroma above rows: U P@7 A@8..15, V P@23 A@24..31
-constexpr int kColY = 1104;   // B_PRED: luma columns 11, 7, 3 of the MB (16 B each, in that order),
+constexpr int kTP = 40;       // tile row pitch: 10 dwords, so that 16 consecutive rows (the lanes of
+                              // a vertical-edge or block pass) fall on 16 different LDS banks
+constexpr int kLfY = 0;       // luma filter tile: 20 rows x kTP (4 rows above + 16 MB rows; two MB
+                              // columns as a ring at +0 / +16, slot = mb_col & 1)
+constexpr int kLfUV = 800;    // chroma tile: 12 rows x kTP (4 above + 8 MB rows); per row U at +0,
+                              // V at +16, each a ring of two 8-B MB columns
+constexpr int kAbY = 1280;    // luma above row: [15] corner P, [16..31] A, [32..35] above-right
+constexpr int kAbUV = 1328;   // chroma above rows: U P@7 A@8..15, V P@23 A@24..31
+constexpr int kColY = 1360;   // B_PRED: luma columns 11, 7, 3 of the MB (16 B each, in that order),
                               // so that the left column of sub-block column j is at kLeft - 16 j
-constexpr int kLeft = 1152;   // unfiltered left columns: Y 0..15, U 16..23, V 24..31
-constexpr int kResid = 1184;  // residual of the MB: 25 blocks (16 Y, 4 U, 4 V, Y2 slot) x 16 int16
-constexpr int kWht = 1984;    // 16 int16 luma DCs out of the inverse WHT
-constexpr int kHalfBytes = 2016;
+constexpr int kLeft = 1408;   // unfiltered left columns: Y 0..15, U 16..23, V 24..31
+constexpr int kResid = 1440;  // residual of the MB: 25 blocks (16 Y, 4 U, 4 V, Y2 slot) x 16 int16
+constexpr int kWht = 2240;    // 16 int16 luma DCs out of the inverse WHT
+constexpr int kHalfBytes = 2272;
 constexpr int kWaveBytes = 2 * kHalfBytes;
 
 // Workgroup header.

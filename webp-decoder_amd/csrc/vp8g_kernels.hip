@@ -64,7 +64,8 @@ namespace {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(1))) u32x4 gu32x4;  // global-memory vector (never flat)
+typedef __attribute__((address_space(1))) u32x4 gu32x4;
+constexpr int kBS = 4 * kTP - 8;  // B_PRED: tile offset from sub-block (i, j) to (i + 1, j - 2)  // global-memory vector (never flat)
 
 // ---------------------------------------------------------------------------------------------
 // B_PRED predictor table (RFC 6386 12.3; reference vp8_recon.c:218-358).  A lane predicting one
@@ -341,7 +342,7 @@ DEV void lf_mb(uint8_t* tY, uint8_t* tC, int ln, int slot, bool en, bool mb_v, b
 	{
 		// (ldb/stb: relaxed wave-scope atomics keep the byte accesses single ds_read_u8 /
 		// ds_write_b8 -- merged wide accesses cost vector instructions to (un)pack)
-		uint8_t* const rowp = isy ? tY + (4 + ln) * 32 : tC + (4 + (ln & 7)) * 32 + cp * 16;
+		uint8_t* const rowp = isy ? tY + (4 + ln) * kTP : tC + (4 + (ln & 7)) * kTP + cp * 16;
 		const int off = isy ? slot * 16 : slot * 8, ring = isy ? 31 : 15;
 		uint8_t* const Lp = rowp + ((off - 4) & ring);
 		uint8_t* const Mp = rowp + off;
@@ -362,18 +363,18 @@ DEV void lf_mb(uint8_t* tY, uint8_t* tC, int ln, int slot, bool en, bool mb_v, b
 		}
 	}
 	wave_lds_sync();
-	// horizontal edges: one line per lane down a pixel column (tile rows 0..19, pitch 32)
+	// horizontal edges: one line per lane down a pixel column (tile rows 0..19, pitch kTP)
 	{
 		uint8_t* const colp = isy ? tY + slot * 16 + ln : tC + cp * 16 + slot * 8 + (ln & 7);
 #pragma unroll
-		for (int i = 0; i < 20; i++) px[i] = ldb(colp + 32 * i);
+		for (int i = 0; i < 20; i++) px[i] = ldb(colp + kTP * i);
 		lf_line<kSimple>(px, en && mb_h, en && inner, isy, E, I, T);
 		if (wr) {
 #pragma unroll
-			for (int i = 1; i < 10; i++) stb(colp + 32 * i, px[i]);
+			for (int i = 1; i < 10; i++) stb(colp + kTP * i, px[i]);
 			if (isy) {
 #pragma unroll
-				for (int i = 10; i < 18; i++) stb(colp + 32 * i, px[i]);
+				for (int i = 10; i < 18; i++) stb(colp + kTP * i, px[i]);
 			}
 		}
 	}
@@ -485,7 +486,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			const int slot = c & 1;
 			uint8_t* const hv = smem + kHdrBytes + wave * kWaveBytes + hh * kHalfBytes;  // this half's area
 			uint8_t* const tY = hv + kLfY;
-			uint8_t* const tC = hv + kLfUV;  // chroma: U at +0, V at +16, row pitch 32
+			uint8_t* const tC = hv + kLfUV;  // chroma: U at +0, V at +16, row pitch kTP
 			uint8_t* const abY = hv + kAbY;
 			uint8_t* const abUV = hv + kAbUV;
 			uint8_t* const left = hv + kLeft;
@@ -613,11 +614,13 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					const uint8_t* src = A.src;
 					if (ln < 16) {
 						const uint8_t* s = src + D.src_y + (size_t)(y0 + ln) * D.src_stride_y + x0;
-						st128(tY + (4 + ln) * 32 + slot * 16, u32x4{ld32(s), ld32(s + 4), ld32(s + 8), ld32(s + 12)});
+						uint8_t* const td = tY + (4 + ln) * kTP + slot * 16;
+						st64(td, u32x2{ld32(s), ld32(s + 4)});
+						st64(td + 8, u32x2{ld32(s + 8), ld32(s + 12)});
 					} else {
 						const int p = (ln - 16) >> 3, row = ln & 7;
 						const uint8_t* s = src + (p ? D.src_v : D.src_u) + (size_t)(cy0 + row) * D.src_stride_uv + cx0;
-						st64(tC + p * 16 + (4 + row) * 32 + slot * 8, u32x2{ld32(s), ld32(s + 4)});
+						st64(tC + p * 16 + (4 + row) * kTP + slot * 8, u32x2{ld32(s), ld32(s + 4)});
 					}
 				} else {
 					// ln 0..3 luma above row, 4 luma above-right (cols x+16..x+19, clamped to the
@@ -642,7 +645,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					const bool ly = ln < 24;
 					const int p = (ln - 24) >> 2, tr = ly ? ln - 20 : (ln - 24) & 3;
 					const uint32_t lo = lf_off(cu) + (ly ? tr * 16 : 64 + p * 32 + tr * 8);
-					uint8_t* const td = ly ? tY + tr * 32 + slot * 16 : tC + p * 16 + tr * 32 + slot * 8;
+					uint8_t* const td = ly ? tY + tr * kTP + slot * 16 : tC + p * 16 + tr * kTP + slot * 8;
 					st64(td, ctx.rd64(lo));
 					if (ly) st64(td + 8, ctx.rd64(lo + 8));
 				}
@@ -678,8 +681,8 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					const uint32_t mA = (mode == 1 || mode == 3) ? 0xFFu : 0u;
 					const uint32_t mL = (mode == 2 || mode == 3) ? 0xFFu : 0u;
 					const int K = (mode == 3 ? -P : 0) + (mode == 0 ? dcv : 0);
-					uint8_t* dst = yl ? tY + (4 + 4 * by) * 32 + slot * 16 + 4 * bx
-					                  : tC + p * 16 + (4 + 4 * by) * 32 + slot * 8 + 4 * bx;
+					uint8_t* dst = yl ? tY + (4 + 4 * by) * kTP + slot * 16 + 4 * bx
+					                  : tC + p * 16 + (4 + 4 * by) * kTP + slot * 8 + 4 * bx;
 					const u32x4 r01 = ld128(hv + kResid + ln * 32), r23 = ld128(hv + kResid + ln * 32 + 16);
 					const uint32_t rw[8] = {r01.x, r01.y, r01.z, r01.w, r23.x, r23.y, r23.z, r23.w};
 					int acol[4];
@@ -694,7 +697,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 							const int rv = (int)(int16_t)((rw[(4 * rr + cc) >> 1] >> (16 * (cc & 1))) & 0xFFFFu);
 							px4[cc] = sat8(sat8(L + acol[cc]) + rv);
 						}
-						st32(dst + rr * 32, pack4(px4[0], px4[1], px4[2], px4[3]));
+						st32(dst + rr * kTP, pack4(px4[0], px4[1], px4[2], px4[3]));
 					}
 				}
 				wave_lds_sync();
@@ -716,8 +719,8 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					                        (uint32_t)rdlane((int)cur.a.z, 57), (uint32_t)rdlane((int)cur.a.w, 57)};
 					const u32x4 bmw = hh ? bm1 : bm0;
 					const int g = (ln >> 4) & 1, p = ln & 15, rr = p >> 2, cc = p & 3;
-					uint8_t* const tpix = tY + slot * 16 + 4 * 32 + 120 * g + 32 * rr + cc;  // + 120 i0 + 4 s
-					const uint8_t* const tA = tY + slot * 16 + 3 * 32 + 120 * g;             // + 120 i0 + 4 s
+					uint8_t* const tpix = tY + slot * 16 + 4 * kTP + kBS * g + kTP * rr + cc;  // + kBS i0 + 4 s
+					const uint8_t* const tA = tY + slot * 16 + 3 * kTP + kBS * g;             // + kBS i0 + 4 s
 					const uint8_t* const aE = g ? tA : abY + 16;                              // i0 == 0: + 4 s
 					uint8_t* const lB = left + 36 * g;                                        // + 36 i0 - 16 s
 					const int16_t* const rsp = (const int16_t*)(hv + kResid) + p + 32 * g;    // + 16 b0
@@ -734,7 +737,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 							const int mb0 = v0 ? (int)((bmw[b0 >> 2] >> (8 * (b0 & 3))) & 0xFFu) : 0;
 							const int mb1 = v1 ? (int)((bmw[(b0 + 2) >> 2] >> (8 * ((b0 + 2) & 3))) & 0xFFu) : 0;
 							const int mode = min(g ? mb1 : mb0, kBpModes - 1);
-							const uint8_t* const arow = i0 == 0 ? aE + 4 * s : tA + 120 * i0 + 4 * s;
+							const uint8_t* const arow = i0 == 0 ? aE + 4 * s : tA + kBS * i0 + 4 * s;
 							// above-right: the MB above's row when this sub-block is in column 3
 							const bool r3_0 = j0 == 3, r3_1 = j0 == 5;
 							const uint8_t* const a47p = (r3_0 || r3_1) ? ((g ? r3_1 : r3_0) ? abY + 32 : arow + 4) : arow + 4;
@@ -753,7 +756,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 							const int vdc = (int)((__builtin_amdgcn_sad_u8(a03, 0u, __builtin_amdgcn_sad_u8(lw, 0u, 4u))) >> 3);
 							const int pred = mode == 0 ? vdc : (mode == 1 ? vtm : vt);
 							const int px = sat8(pred + rv);
-							tpix[120 * i0 + 4 * s] = (uint8_t)px;
+							tpix[kBS * i0 + 4 * s] = (uint8_t)px;
 							// right pixel column of a sub-block: left column of the next sub-block column
 							const bool w3 = (g ? j0 - 2 : j0) < 3;
 							if (col3 && w3) lb[-16 + rr] = (uint8_t)px;
@@ -768,12 +771,15 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			// ---------------------------------------------- save unfiltered context
 			if (act && !lf_only) {
 				// right column -> left column of the next MB (Y 16, U 8, V 8 lanes)
-				const uint8_t* sp = ln < 16 ? tY + (4 + ln) * 32 + slot * 16 + 15
-				                            : tC + ((ln >> 3) & 1) * 16 + (4 + (ln & 7)) * 32 + slot * 8 + 7;
+				const uint8_t* sp = ln < 16 ? tY + (4 + ln) * kTP + slot * 16 + 15
+				                            : tC + ((ln >> 3) & 1) * 16 + (4 + (ln & 7)) * kTP + slot * 8 + 7;
 				const uint8_t pxv = *sp;
-				if (ln == 0) ctx.wr128(rec_off(cu), ld128(tY + 19 * 32 + slot * 16));  // bottom rows -> ctx_rec[c]
-				else if (ln == 1) ctx.wr64(rec_off(cu) + 16, ld64(tC + 11 * 32 + slot * 8));
-				else if (ln == 2) ctx.wr64(rec_off(cu) + 24, ld64(tC + 16 + 11 * 32 + slot * 8));
+				if (ln == 0) {  // bottom rows -> ctx_rec[c]
+					ctx.wr64(rec_off(cu), ld64(tY + 19 * kTP + slot * 16));
+					ctx.wr64(rec_off(cu) + 8, ld64(tY + 19 * kTP + slot * 16 + 8));
+				}
+				else if (ln == 1) ctx.wr64(rec_off(cu) + 16, ld64(tC + 11 * kTP + slot * 8));
+				else if (ln == 2) ctx.wr64(rec_off(cu) + 24, ld64(tC + 16 + 11 * kTP + slot * 8));
 				else if (ln == 3) {  // corner for the next MB
 					abY[15] = abY[31];
 					abUV[7] = abUV[15];
@@ -824,7 +830,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			if (!lf_on) {
 				// unfiltered: MB(r, c) is final as soon as it is reconstructed
 				const int pl = ln < 16 ? 0 : ((ln - 16) >> 3) + 1, row = ln < 16 ? ln : (ln & 7);
-				const uint8_t* src = ln < 16 ? tY + (4 + ln) * 32 + slot * 16 : tC + (pl - 1) * 16 + (4 + row) * 32 + slot * 8;
+				const uint8_t* src = ln < 16 ? tY + (4 + ln) * kTP + slot * 16 : tC + (pl - 1) * 16 + (4 + row) * kTP + slot * 8;
 				emit(act, pl, (ln < 16 ? y0 : cy0) + row, cu, src);
 			} else {
 				const bool last_row = r + 1 == R;
@@ -840,7 +846,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					const int sl = slot ^ prev;
 					// tile row: top strip 0..3, body 4.., tail 16.. (luma) / 8.. (chroma); image row = base + trow - 4
 					const int trow = kind == 0 ? kk : (kind == 1 ? 4 + kk : (isy ? 16 : 8) + kk);
-					const uint8_t* src = isy ? tY + trow * 32 + sl * 16 : tC + (pl - 1) * 16 + trow * 32 + sl * 8;
+					const uint8_t* src = isy ? tY + trow * kTP + sl * 16 : tC + (pl - 1) * 16 + trow * kTP + sl * 8;
 					const bool to_ctx = ok && kind == 2 && !last_row;
 					if (to_ctx) {
 						const uint32_t off = lf_off(col) + (isy ? kk * 16 : 64 + (pl - 1) * 32 + kk * 8);
