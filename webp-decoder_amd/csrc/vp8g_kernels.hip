@@ -129,45 +129,6 @@ constexpr BpTab make_bptab() {
 }
 __constant__ BpTab kBpTab = make_bptab();
 
-// ---------------------------------------------------------------------------------------------
-// Store tasks of the loop-filter flush, per (round, lane-in-half).  Entry: bit15 valid,
-// [9:8] plane (0 Y, 1 U, 2 V), [7:6] kind (0 = top strip = the MB above's rows 12..15 (Y) /
-// 4..7 (UV), final now; 1 = body rows 0..11 / 0..3, final once this MB's left edge ran;
-// 2 = tail rows 12..15 / 4..7, handed to the row below through ctx_lf), bit5 which MB (0 cur,
-// 1 the previous column), [3:0] row within the group.
-// ---------------------------------------------------------------------------------------------
-struct FlushTab {
-	uint16_t v[96];
-};
-constexpr uint16_t FT(int plane, int kind, int prev, int k) {
-	return (uint16_t)(0x8000 | (plane << 8) | (kind << 6) | (prev << 5) | k);
-}
-constexpr FlushTab make_flushtab() {
-	FlushTab t{};
-	for (int ln = 0; ln < 32; ln++) {
-		uint16_t e0 = 0, e1 = 0, e2 = 0;
-		if (ln < 4) e0 = FT(0, 0, 0, ln);
-		else if (ln < 16) e0 = FT(0, 1, 1, ln - 4);
-		else if (ln < 20) e0 = FT(0, 2, 1, ln - 16);
-		else if (ln < 24) e0 = FT(1, 0, 0, ln - 20);
-		else if (ln < 28) e0 = FT(2, 0, 0, ln - 24);
-		else e0 = FT(1, 1, 1, ln - 28);
-		if (ln < 4) e1 = FT(2, 1, 1, ln);
-		else if (ln < 8) e1 = FT(1, 2, 1, ln - 4);
-		else if (ln < 12) e1 = FT(2, 2, 1, ln - 8);
-		else if (ln < 24) e1 = FT(0, 1, 0, ln - 12);
-		else if (ln < 28) e1 = FT(0, 2, 0, ln - 24);
-		else e1 = FT(1, 1, 0, ln - 28);
-		if (ln < 4) e2 = FT(2, 1, 0, ln);
-		else if (ln < 8) e2 = FT(1, 2, 0, ln - 4);
-		else if (ln < 12) e2 = FT(2, 2, 0, ln - 8);
-		t.v[ln] = e0;
-		t.v[32 + ln] = e1;
-		t.v[64 + ln] = e2;
-	}
-	return t;
-}
-__constant__ FlushTab kFlushTab = make_flushtab();
 
 // ---------------------------------------------------------------------------------------------
 // small helpers
@@ -405,7 +366,6 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 	const Vp8gFrameDesc& D = descs[f];
 
 	for (int i = (int)threadIdx.x; i < kBpModes * 32; i += NW * 64) ((uint32_t*)(smem + kBpTable))[i] = kBpTab.v[i];
-	for (int i = (int)threadIdx.x; i < 96; i += NW * 64) ((uint16_t*)(smem + kFlushTable))[i] = kFlushTab.v[i];
 	if (threadIdx.x < 24) ((int16_t*)(smem + kDqTable))[threadIdx.x] = D.dq[threadIdx.x / 6][threadIdx.x % 6];
 	if (threadIdx.x < 32) smem[kLfTable + threadIdx.x] = D.lf[threadIdx.x >> 3][(threadIdx.x >> 2) & 1][threadIdx.x & 3];
 	if (threadIdx.x < 16) ((uint32_t*)(smem + kProgress))[threadIdx.x] = 0;
@@ -519,32 +479,31 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 				uint32_t w[8] = {pk_mul(cur.a.x, fdcac), pk_mul(cur.a.y, facac), pk_mul(cur.a.z, facac), pk_mul(cur.a.w, facac),
 				                 pk_mul(cur.b.x, facac), pk_mul(cur.b.y, facac), pk_mul(cur.b.z, facac), pk_mul(cur.b.w, facac)};
 				const bool anyac = ((w[0] >> 16) | w[1] | w[2] | w[3] | w[4] | w[5] | w[6] | w[7]) != 0u;
-				// Y2 (non-B_PRED): inverse WHT (RFC 14.3) in the Y2 lane, 16 DCs to LDS
+				// Y2 (non-B_PRED): inverse WHT (RFC 14.3), 16 DCs to LDS.  Lanes 26..29 hold the Y2
+				// coefficients too (their prefetch duplicates lane 24's load): the vertical pass runs
+				// packed in lanes 26 / 27 (column pairs 0-1 / 2-3), the horizontal pass one row per
+				// lane in 26..29, through kWht.
 				if (__ballot(act && !bpred) != 0ull) {
-					if (ln == 24 && act && !bpred) {
-						int v[16], t2[16], o[16];
-#pragma unroll
-						for (int i = 0; i < 16; i++) v[i] = lo_s16(w[i >> 1] >> (16 * (i & 1)));
-#pragma unroll
-						for (int i = 0; i < 4; i++) {
-							const int a1 = v[i] + v[12 + i], b1 = v[4 + i] + v[8 + i];
-							const int c1 = v[4 + i] - v[8 + i], d1 = v[i] - v[12 + i];
-							t2[i] = sx16(a1 + b1);
-							t2[4 + i] = sx16(c1 + d1);
-							t2[8 + i] = sx16(a1 - b1);
-							t2[12 + i] = sx16(d1 - c1);
+					const bool wl = ln >= 26 && ln < 30;
+					{
+						const int h = ln & 1;
+						const uint32_t r0 = h ? w[1] : w[0], r1 = h ? w[3] : w[2], r2 = h ? w[5] : w[4], r3 = h ? w[7] : w[6];
+						const uint32_t a1 = pk_add(r0, r3), b1 = pk_add(r1, r2), c1 = pk_sub(r1, r2), d1 = pk_sub(r0, r3);
+						if (ln == 26 || ln == 27) {
+							uint8_t* const q = hv + kWht + 4 * h;
+							st32(q, pk_add(a1, b1));
+							st32(q + 8, pk_add(c1, d1));
+							st32(q + 16, pk_sub(a1, b1));
+							st32(q + 24, pk_sub(d1, c1));
 						}
-#pragma unroll
-						for (int i = 0; i < 4; i++) {
-							const int* q = t2 + 4 * i;
-							const int a1 = q[0] + q[3], b1 = q[1] + q[2], c1 = q[1] - q[2], d1 = q[0] - q[3];
-							o[4 * i + 0] = (a1 + b1 + 3) >> 3;
-							o[4 * i + 1] = (c1 + d1 + 3) >> 3;
-							o[4 * i + 2] = (a1 - b1 + 3) >> 3;
-							o[4 * i + 3] = (d1 - c1 + 3) >> 3;
-						}
-						st128(hv + kWht, u32x4{pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7])});
-						st128(hv + kWht + 16, u32x4{pack2(o[8], o[9]), pack2(o[10], o[11]), pack2(o[12], o[13]), pack2(o[14], o[15])});
+					}
+					wave_lds_sync();
+					if (wl) {
+						uint8_t* const q = hv + kWht + 8 * (ln - 26);
+						const u32x2 t = ld64(q);
+						const int q0 = lo_s16(t.x), q1 = hi_s16(t.x), q2 = lo_s16(t.y), q3 = hi_s16(t.y);
+						const int a1 = q0 + q3 + 3, b1 = q1 + q2, c1 = q1 - q2, d1 = q0 - q3 + 3;
+						st64(q, u32x2{pack2((a1 + b1) >> 3, (c1 + d1) >> 3), pack2((a1 - b1) >> 3, (d1 - c1) >> 3)});
 					}
 					wave_lds_sync();
 					if (ln < 16 && !bpred) w[0] = (w[0] & 0xFFFF0000u) | *(const uint16_t*)(hv + kWht + 2 * ln);
@@ -807,53 +766,78 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			// One row piece per lane (luma 16 B, chroma 8 B) from LDS to the output plane or, for the
 			// bottom rows the next MB row still filters, to ctx_lf.  Straight-line: the crop / odd
 			// alignment case (a partial row piece at the right edge) is a rare wave-uniform branch.
-			auto emit = [&](bool ok, int pl, uint32_t prow, uint32_t col, const uint8_t* src) {
-				const bool isy = pl == 0;
-				const u32x2 lo = ld64(src), hi = ld64(src + 8);  // hi: luma only
-				const uint32_t colpx = col * (isy ? 16u : 8u), nb = isy ? 16u : 8u;
-				uint8_t* const plane = isy ? outY : (pl == 2 ? outV : outU);
-				uint8_t* const d = plane + (size_t)prow * (isy ? sy : suv) + colpx;
-				const bool vis = ok && prow < (isy ? H : CH) && !(VP8G_ABLATE & 4);
-				const uint32_t vw = isy ? W : CW;
-				const bool full = colpx + nb <= vw && (((uintptr_t)d) & (nb - 1)) == 0;
-				if (vis && full) {
-					if (isy) *(u32x4*)d = u32x4{lo.x, lo.y, hi.x, hi.y};
-					else *(u32x2*)d = lo;
-				}
+			// Rounds are plane-uniform (luma 16-B pieces / chroma 8-B pieces), so plane pointers,
+			// strides and crop limits stay scalar.
+			auto emitY = [&](bool ok, uint32_t prow, uint32_t col, const uint8_t* src) {
+				const u32x2 lo = ld64(src), hi = ld64(src + 8);
+				const uint32_t colpx = col * 16u;
+				uint8_t* const d = outY + (size_t)prow * sy + colpx;
+				const bool vis = ok && prow < H && !(VP8G_ABLATE & 4);
+				const bool full = colpx + 16u <= W && (((uintptr_t)d) & 15u) == 0;
+				if (vis && full) *(u32x4*)d = u32x4{lo.x, lo.y, hi.x, hi.y};
 				if (__ballot(vis && !full) != 0ull) {
 					if (vis && !full) {
-						const uint32_t n = vw - colpx, cnt = n < nb ? n : nb;
+						const uint32_t n = W - colpx, cnt = n < 16u ? n : 16u;
+						for (uint32_t q = 0; q < cnt; q++) d[q] = src[q];
+					}
+				}
+			};
+			auto emitC = [&](bool ok, int p, uint32_t prow, uint32_t col, const uint8_t* src) {
+				const u32x2 lo = ld64(src);
+				const uint32_t colpx = col * 8u;
+				uint8_t* const d = (p ? outV : outU) + (size_t)prow * suv + colpx;
+				const bool vis = ok && prow < CH && !(VP8G_ABLATE & 4);
+				const bool full = colpx + 8u <= CW && (((uintptr_t)d) & 7u) == 0;
+				if (vis && full) *(u32x2*)d = lo;
+				if (__ballot(vis && !full) != 0ull) {
+					if (vis && !full) {
+						const uint32_t n = CW - colpx, cnt = n < 8u ? n : 8u;
 						for (uint32_t q = 0; q < cnt; q++) d[q] = src[q];
 					}
 				}
 			};
 			if (!lf_on) {
 				// unfiltered: MB(r, c) is final as soon as it is reconstructed
-				const int pl = ln < 16 ? 0 : ((ln - 16) >> 3) + 1, row = ln < 16 ? ln : (ln & 7);
-				const uint8_t* src = ln < 16 ? tY + (4 + ln) * kTP + slot * 16 : tC + (pl - 1) * 16 + (4 + row) * kTP + slot * 8;
-				emit(act, pl, (ln < 16 ? y0 : cy0) + row, cu, src);
+				if (ln < 16) emitY(act, y0 + ln, cu, tY + (4 + ln) * kTP + slot * 16);
+				else {
+					const int p = (ln - 16) >> 3, row = ln & 7;
+					emitC(act, p, cy0 + row, cu, tC + p * 16 + (4 + row) * kTP + slot * 8);
+				}
 			} else {
 				const bool last_row = r + 1 == R;
-				const bool last_col = cu + 1 == C;
-				const uint16_t* ftab = (const uint16_t*)(smem + kFlushTable);
-				const int rounds = __ballot(act && last_col) != 0ull ? 3 : 2;
-				for (int rd = 0; rd < rounds; rd++) {
-					const uint32_t e = ftab[rd * 32 + ln];
-					const int pl = (e >> 8) & 3, kind = (e >> 6) & 3, prev = (e >> 5) & 1, kk = e & 15;
-					const bool ok = act && (e & 0x8000u) && (kind != 0 || r > 0) && (prev ? c > 0 : (kind == 0 || last_col));
-					const bool isy = pl == 0;
-					const uint32_t col = prev ? cu - 1 : cu;
-					const int sl = slot ^ prev;
-					// tile row: top strip 0..3, body 4.., tail 16.. (luma) / 8.. (chroma); image row = base + trow - 4
-					const int trow = kind == 0 ? kk : (kind == 1 ? 4 + kk : (isy ? 16 : 8) + kk);
-					const uint8_t* src = isy ? tY + trow * kTP + sl * 16 : tC + (pl - 1) * 16 + trow * kTP + sl * 8;
-					const bool to_ctx = ok && kind == 2 && !last_row;
+				// tile row t of a column holds image row (MB row origin) + t - 4; rows >= 16 (luma) /
+				// >= 8 (chroma) are the bottom 4 rows the next MB row still filters: to ctx_lf unless
+				// this is the last MB row
+				auto flushY = [&](bool ok, int trow, uint32_t col, int sl) {
+					const uint8_t* src = tY + trow * kTP + sl * 16;
+					const bool to_ctx = ok && trow >= 16 && !last_row;
 					if (to_ctx) {
-						const uint32_t off = lf_off(col) + (isy ? kk * 16 : 64 + (pl - 1) * 32 + kk * 8);
+						const uint32_t off = lf_off(col) + (trow - 16) * 16;
 						ctx.wr64(off, ld64(src));
-						if (isy) ctx.wr64(off + 8, ld64(src + 8));
+						ctx.wr64(off + 8, ld64(src + 8));
 					}
-					emit(ok && !to_ctx, pl, (isy ? y0 : cy0) + trow - 4, col, src);
+					emitY(ok && !to_ctx, y0 + trow - 4, col, src);
+				};
+				auto flushC = [&](bool ok, int p, int trow, uint32_t col, int sl) {
+					const uint8_t* src = tC + p * 16 + trow * kTP + sl * 8;
+					const bool to_ctx = ok && trow >= 8 && !last_row;
+					if (to_ctx) ctx.wr64(lf_off(col) + 64 + p * 32 + (trow - 8) * 8, ld64(src));
+					emitC(ok && !to_ctx, p, cy0 + trow - 4, col, src);
+				};
+				{  // luma: ln 0..3 the MB above's bottom rows (this column, final now); 4..19 the left MB
+					const bool top = ln < 4;
+					flushY(act && ln < 20 && (top ? r > 0 : c > 0), ln, top ? cu : cu - 1, top ? slot : slot ^ 1);
+				}
+				{  // chroma: plane ln / 12, tile row ln % 12 (same split)
+					const int p = ln >= 12 ? 1 : 0, k = ln - 12 * p;
+					const bool top = k < 4;
+					flushC(act && ln < 24 && (top ? r > 0 : c > 0), p, k, top ? cu : cu - 1, top ? slot : slot ^ 1);
+				}
+				SUBMARK(21);
+				if (__ballot(act && cu + 1 == C) != 0ull) {  // last column: its own rows are final too
+					const bool own = act && cu + 1 == C;
+					flushY(own && ln < 16, 4 + ln, cu, slot);
+					flushC(own && ln < 16, ln >> 3, 4 + (ln & 7), cu, slot);
 				}
 			}
 			wave_lds_sync();
