@@ -290,6 +290,46 @@ DEV void lf_line(int* px, bool mb_edge, bool inner, bool is_y, int E, int I, int
 	}
 }
 
+// Gather 20 bytes from LDS into 20 VGPRs: px[0..3] = a[0..3], px[4..19] = b[o .. o + 15*st] (byte
+// loads at immediate offsets in one asm block that ends with its own lgkmcnt wait; separate C++
+// loads get merged into wide loads plus unpacking, or carry a zero-extension per byte)
+template <int kA, int kB>  // byte pitch of the a-run and the b-run
+DEV void gather20(const uint8_t* a, const uint8_t* b, int* px) {
+	const uint32_t la = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)a;
+	const uint32_t lb = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)b;
+#define G1(i, base, off) "ds_read_u8 %" #i ", %" base " offset:" #off "\n"
+	asm volatile(
+	    "ds_read_u8 %0, %20\n"
+	    "ds_read_u8 %1, %20 offset:%22\n"
+	    "ds_read_u8 %2, %20 offset:%23\n"
+	    "ds_read_u8 %3, %20 offset:%24\n"
+	    "ds_read_u8 %4, %21\n"
+	    "ds_read_u8 %5, %21 offset:%25\n"
+	    "ds_read_u8 %6, %21 offset:%26\n"
+	    "ds_read_u8 %7, %21 offset:%27\n"
+	    "ds_read_u8 %8, %21 offset:%28\n"
+	    "ds_read_u8 %9, %21 offset:%29\n"
+	    "ds_read_u8 %10, %21 offset:%30\n"
+	    "ds_read_u8 %11, %21 offset:%31\n"
+	    "ds_read_u8 %12, %21 offset:%32\n"
+	    "ds_read_u8 %13, %21 offset:%33\n"
+	    "ds_read_u8 %14, %21 offset:%34\n"
+	    "ds_read_u8 %15, %21 offset:%35\n"
+	    "ds_read_u8 %16, %21 offset:%36\n"
+	    "ds_read_u8 %17, %21 offset:%37\n"
+	    "ds_read_u8 %18, %21 offset:%38\n"
+	    "ds_read_u8 %19, %21 offset:%39\n"
+	    "s_waitcnt lgkmcnt(0)"
+	    : "=&v"(px[0]), "=&v"(px[1]), "=&v"(px[2]), "=&v"(px[3]), "=&v"(px[4]), "=&v"(px[5]), "=&v"(px[6]),
+	      "=&v"(px[7]), "=&v"(px[8]), "=&v"(px[9]), "=&v"(px[10]), "=&v"(px[11]), "=&v"(px[12]), "=&v"(px[13]),
+	      "=&v"(px[14]), "=&v"(px[15]), "=&v"(px[16]), "=&v"(px[17]), "=&v"(px[18]), "=&v"(px[19])
+	    : "v"(la), "v"(lb), "i"(kA), "i"(2 * kA), "i"(3 * kA), "i"(kB), "i"(2 * kB), "i"(3 * kB), "i"(4 * kB),
+	      "i"(5 * kB), "i"(6 * kB), "i"(7 * kB), "i"(8 * kB), "i"(9 * kB), "i"(10 * kB), "i"(11 * kB), "i"(12 * kB),
+	      "i"(13 * kB), "i"(14 * kB), "i"(15 * kB)
+	    : "memory");
+#undef G1
+}
+
 // Both passes of the loop filter over this lane's line of the MB held in LDS.  Lanes 0..15:
 // luma rows / columns; 16..23 U, 24..31 V.  Bytes that may change: 1..17 (luma), 1..9 (chroma).
 template <bool kSimple>
@@ -307,10 +347,7 @@ DEV void lf_mb(uint8_t* tY, uint8_t* tC, int ln, int slot, bool en, bool mb_v, b
 		const int off = isy ? slot * 16 : slot * 8, ring = isy ? 31 : 15;
 		uint8_t* const Lp = rowp + ((off - 4) & ring);
 		uint8_t* const Mp = rowp + off;
-#pragma unroll
-		for (int i = 0; i < 4; i++) px[i] = ldb(Lp + i);
-#pragma unroll
-		for (int i = 0; i < 16; i++) px[4 + i] = ldb(Mp + i);
+		gather20<1, 1>(Lp, Mp, px);
 		lf_line<kSimple>(px, en && mb_v, en && inner, isy, E, I, T);
 		if (wr) {
 #pragma unroll
@@ -327,8 +364,7 @@ DEV void lf_mb(uint8_t* tY, uint8_t* tC, int ln, int slot, bool en, bool mb_v, b
 	// horizontal edges: one line per lane down a pixel column (tile rows 0..19, pitch kTP)
 	{
 		uint8_t* const colp = isy ? tY + slot * 16 + ln : tC + cp * 16 + slot * 8 + (ln & 7);
-#pragma unroll
-		for (int i = 0; i < 20; i++) px[i] = ldb(colp + kTP * i);
+		gather20<kTP, kTP>(colp, colp + 4 * kTP, px);
 		lf_line<kSimple>(px, en && mb_h, en && inner, isy, E, I, T);
 		if (wr) {
 #pragma unroll
