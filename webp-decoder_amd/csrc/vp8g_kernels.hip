@@ -215,8 +215,9 @@ struct Ctx {
 		if constexpr (kG) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 	}
 };
-DEV uint32_t rec_off(uint32_t c) { return c * kCtxBytesPerCol; }
-DEV uint32_t lf_off(uint32_t c) { return c * kCtxBytesPerCol + kCtxRecBytes; }
+// (24-bit multiplies: v_mul_lo_u32 is a quarter-rate instruction; all operands here are < 2^24)
+DEV uint32_t rec_off(uint32_t c) { return __umul24(c, (uint32_t)kCtxBytesPerCol); }
+DEV uint32_t lf_off(uint32_t c) { return __umul24(c, (uint32_t)kCtxBytesPerCol) + kCtxRecBytes; }
 
 // ---------------------------------------------------------------------------------------------
 // Loop filter on a line of pixels (RFC 6386 15.2-15.4; reference vp8_loopfilter.c:24-164),
@@ -238,7 +239,7 @@ DEV void lf_mb_edge(int* x, bool en, int lim, int I, int T) {  // normal, MB edg
 	bool m, hev;
 	edge_mask(x, en, lim, I, T, m, hev);
 	const int p2 = x[1], p1 = x[2], p0 = x[3], q0 = x[4], q1 = x[5], q2 = x[6];
-	const int w = sclamp(sclamp(p1 - q1) + 3 * (q0 - p0));
+	const int w = sclamp(sclamp(p1 - q1) + __mul24(q0 - p0, 3));
 	const int f1 = sclamp(w + 4) >> 3, f2 = sclamp(w + 3) >> 3;
 	const int a27 = (27 * w + 63) >> 7, a18 = (18 * w + 63) >> 7, a9 = (9 * w + 63) >> 7;
 	const bool mh = m & hev, mn = m & !hev;
@@ -255,7 +256,7 @@ DEV void lf_sub_edge(int* x, bool en, int lim, int I, int T) {  // normal, sub-b
 	bool m, hev;
 	edge_mask(x, en, lim, I, T, m, hev);
 	const int p1 = x[2], p0 = x[3], q0 = x[4], q1 = x[5];
-	const int a = sclamp(3 * (q0 - p0) + (hev ? sclamp(p1 - q1) : 0));
+	const int a = sclamp(__mul24(q0 - p0, 3) + (hev ? sclamp(p1 - q1) : 0));
 	const int f1 = sclamp(a + 4) >> 3, f2 = sclamp(a + 3) >> 3;
 	const int a2 = (f1 + 1) >> 1;
 	const bool mn = m & !hev;
@@ -268,7 +269,7 @@ DEV void lf_sub_edge(int* x, bool en, int lim, int I, int T) {  // normal, sub-b
 DEV void lf_simple_edge(int* x, bool en, int lim) {  // simple filter (luma only)
 	const int p1 = x[2], p0 = x[3], q0 = x[4], q1 = x[5];
 	const bool m = en & (ad(p0, q0) * 2 + (ad(p1, q1) >> 1) <= lim);
-	const int a = sclamp(sclamp(p1 - q1) + 3 * (q0 - p0));
+	const int a = sclamp(sclamp(p1 - q1) + __mul24(q0 - p0, 3));
 	x[4] = m ? sat8(q0 - (sclamp(a + 4) >> 3)) : q0;
 	x[3] = m ? sat8(p0 + (sclamp(a + 3) >> 3)) : p0;
 }
@@ -328,6 +329,8 @@ DEV void gather20(const uint8_t* a, const uint8_t* b, int* px) {
 	      "i"(13 * kB), "i"(14 * kB), "i"(15 * kB)
 	    : "memory");
 #undef G1
+#pragma unroll
+	for (int i = 0; i < 20; i++) __builtin_assume((uint32_t)px[i] < 256u);  // bytes: lets 24-bit multiplies through
 }
 
 // Both passes of the loop filter over this lane's line of the MB held in LDS.  Lanes 0..15:
@@ -418,6 +421,8 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 	uint8_t* const outV = out + D.out_v;
 	const uint32_t W = D.width, H = D.height, CW = (D.width + 1) >> 1, CH = (D.height + 1) >> 1;
 	const uint32_t sy = D.stride_y, suv = D.stride_uv;
+	const uint32_t vofs = (uint32_t)(D.out_v - D.out_u);  // V plane relative to U (< 2^32 by construction)
+	const uint32_t yal = (uint32_t)(uintptr_t)outY, ual = (uint32_t)(uintptr_t)outU;  // alignment tests
 	uint32_t* const prog = (uint32_t*)(smem + kProgress);
 	Ctx<kG> ctx;
 	ctx.lds = smem + kHdrBytes + NW * kWaveBytes;
@@ -439,7 +444,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 		const int hh = lane >> 5, ln = lane & 31;
 		const int cn = tt - 2 * hh;
 		const bool inb = (hh == 0 || two) && cn >= 0 && cn < (int)C;
-		const uint64_t m = mb0 + (inb ? (uint64_t)((rA + hh) * C + (uint32_t)cn) : 0ull);
+		const uint64_t m = mb0 + (inb ? (uint64_t)(__umul24(rA + hh, C) + (uint32_t)cn) : 0ull);
 		// Issued unconditionally (loop-filter-only frames read the descriptor instead of the
 		// absent coefficient arrays): a path without these loads would make the compiler's
 		// wait-count analysis fall back to vmcnt(0) on the next step's use of the side bytes,
@@ -480,7 +485,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			const bool act = (hh == 0 || two) && c >= 0 && c < (int)C;
 			const uint32_t cu = (uint32_t)c;
 			const int slot = c & 1;
-			uint8_t* const hv = smem + kHdrBytes + wave * kWaveBytes + hh * kHalfBytes;  // this half's area
+			uint8_t* const hv = smem + kHdrBytes + wave * kWaveBytes + (hh ? kHalfBytes : 0);  // this half's area
 			uint8_t* const tY = hv + kLfY;
 			uint8_t* const tC = hv + kLfUV;  // chroma: U at +0, V at +16, row pitch kTP
 			uint8_t* const abY = hv + kAbY;
@@ -804,61 +809,62 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			// alignment case (a partial row piece at the right edge) is a rare wave-uniform branch.
 			// Rounds are plane-uniform (luma 16-B pieces / chroma 8-B pieces), so plane pointers,
 			// strides and crop limits stay scalar.
-			auto emitY = [&](bool ok, uint32_t prow, uint32_t col, const uint8_t* src) {
-				const u32x2 lo = ld64(src), hi = ld64(src + 8);
+			// 32-bit offsets from the (uniform) plane bases, so stores use the SGPR-base address form
+			auto emitY = [&](bool ok, uint32_t prow, uint32_t col, const uint8_t* src, u32x2 lo, u32x2 hi) {
 				const uint32_t colpx = col * 16u;
-				uint8_t* const d = outY + (size_t)prow * sy + colpx;
+				const uint32_t off = __umul24(prow, sy) + colpx;
 				const bool vis = ok && prow < H && !(VP8G_ABLATE & 4);
-				const bool full = colpx + 16u <= W && (((uintptr_t)d) & 15u) == 0;
-				if (vis && full) *(u32x4*)d = u32x4{lo.x, lo.y, hi.x, hi.y};
+				const bool full = colpx + 16u <= W && ((yal + off) & 15u) == 0;
+				if (vis && full) *(u32x4*)(outY + off) = u32x4{lo.x, lo.y, hi.x, hi.y};
 				if (__ballot(vis && !full) != 0ull) {
 					if (vis && !full) {
 						const uint32_t n = W - colpx, cnt = n < 16u ? n : 16u;
-						for (uint32_t q = 0; q < cnt; q++) d[q] = src[q];
+						for (uint32_t q = 0; q < cnt; q++) outY[off + q] = src[q];
 					}
 				}
 			};
-			auto emitC = [&](bool ok, int p, uint32_t prow, uint32_t col, const uint8_t* src) {
-				const u32x2 lo = ld64(src);
+			auto emitC = [&](bool ok, int p, uint32_t prow, uint32_t col, const uint8_t* src, u32x2 lo) {
 				const uint32_t colpx = col * 8u;
-				uint8_t* const d = (p ? outV : outU) + (size_t)prow * suv + colpx;
+				const uint32_t off = (p ? vofs : 0u) + __umul24(prow, suv) + colpx;  // from outU
 				const bool vis = ok && prow < CH && !(VP8G_ABLATE & 4);
-				const bool full = colpx + 8u <= CW && (((uintptr_t)d) & 7u) == 0;
-				if (vis && full) *(u32x2*)d = lo;
+				const bool full = colpx + 8u <= CW && ((ual + off) & 7u) == 0;
+				if (vis && full) *(u32x2*)(outU + off) = lo;
 				if (__ballot(vis && !full) != 0ull) {
 					if (vis && !full) {
 						const uint32_t n = CW - colpx, cnt = n < 8u ? n : 8u;
-						for (uint32_t q = 0; q < cnt; q++) d[q] = src[q];
+						for (uint32_t q = 0; q < cnt; q++) outU[off + q] = src[q];
 					}
 				}
 			};
 			if (!lf_on) {
 				// unfiltered: MB(r, c) is final as soon as it is reconstructed
-				if (ln < 16) emitY(act, y0 + ln, cu, tY + (4 + ln) * kTP + slot * 16);
-				else {
+				if (ln < 16) {
+					const uint8_t* src = tY + (4 + ln) * kTP + slot * 16;
+					emitY(act, y0 + ln, cu, src, ld64(src), ld64(src + 8));
+				} else {
 					const int p = (ln - 16) >> 3, row = ln & 7;
-					emitC(act, p, cy0 + row, cu, tC + p * 16 + (4 + row) * kTP + slot * 8);
+					const uint8_t* src = tC + p * 16 + (4 + row) * kTP + slot * 8;
+					emitC(act, p, cy0 + row, cu, src, ld64(src));
 				}
 			} else {
 				const bool last_row = r + 1 == R;
 				// tile row t of a column holds image row (MB row origin) + t - 4; rows >= 16 (luma) /
 				// >= 8 (chroma) are the bottom 4 rows the next MB row still filters: to ctx_lf unless
 				// this is the last MB row
+				// (the row piece is loaded once, by every lane -- addresses stay inside the half's area)
 				auto flushY = [&](bool ok, int trow, uint32_t col, int sl) {
 					const uint8_t* src = tY + trow * kTP + sl * 16;
+					const u32x2 lo = ld64(src), hi = ld64(src + 8);
 					const bool to_ctx = ok && trow >= 16 && !last_row;
-					if (to_ctx) {
-						const uint32_t off = lf_off(col) + (trow - 16) * 16;
-						ctx.wr64(off, ld64(src));
-						ctx.wr64(off + 8, ld64(src + 8));
-					}
-					emitY(ok && !to_ctx, y0 + trow - 4, col, src);
+					if (to_ctx) ctx.wr128(lf_off(col) + (trow - 16) * 16, u32x4{lo.x, lo.y, hi.x, hi.y});
+					emitY(ok && !to_ctx, y0 + trow - 4, col, src, lo, hi);
 				};
 				auto flushC = [&](bool ok, int p, int trow, uint32_t col, int sl) {
 					const uint8_t* src = tC + p * 16 + trow * kTP + sl * 8;
+					const u32x2 lo = ld64(src);
 					const bool to_ctx = ok && trow >= 8 && !last_row;
-					if (to_ctx) ctx.wr64(lf_off(col) + 64 + p * 32 + (trow - 8) * 8, ld64(src));
-					emitC(ok && !to_ctx, p, cy0 + trow - 4, col, src);
+					if (to_ctx) ctx.wr64(lf_off(col) + 64 + p * 32 + (trow - 8) * 8, lo);
+					emitC(ok && !to_ctx, p, cy0 + trow - 4, col, src, lo);
 				};
 				{  // luma: ln 0..3 the MB above's bottom rows (this column, final now); 4..19 the left MB
 					const bool top = ln < 4;
