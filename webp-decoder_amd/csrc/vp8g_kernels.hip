@@ -129,6 +129,29 @@ constexpr BpTab make_bptab() {
 }
 __constant__ BpTab kBpTab = make_bptab();
 
+// Border setup roles of lanes 0..19 (see "borders"): dst offset in the half area [11:0], source
+// offset in the unfiltered context row [19:12], kind [21:20] (0 above, 1 left fill, 2 corner).
+struct BorderTab {
+	uint32_t v[32];
+};
+constexpr uint32_t BE(int dst, int src, int kind) { return (uint32_t)dst | ((uint32_t)src << 12) | ((uint32_t)kind << 20); }
+constexpr BorderTab make_bordertab() {
+	BorderTab t{};
+	for (int ln = 0; ln < 32; ln++) {
+		if (ln < 4) t.v[ln] = BE(kAbY + 16 + 4 * ln, 4 * ln, 0);
+		else if (ln == 4) t.v[ln] = BE(kAbY + 32, 0, 0);
+		else if (ln < 9) {
+			const int q = ln - 5;
+			t.v[ln] = BE(kAbUV + 8 + 16 * (q >> 1) + 4 * (q & 1), 16 + 8 * (q >> 1) + 4 * (q & 1), 0);
+		} else if (ln < 17) t.v[ln] = BE(kLeft + 4 * (ln - 9), 0, 1);
+		else if (ln == 17) t.v[ln] = BE(kAbY + 12, 0, 2);
+		else if (ln < 20) t.v[ln] = BE(kAbUV + 4 + 16 * (ln - 18), 0, 2);
+		else t.v[ln] = BE(0, 0, 3);
+	}
+	return t;
+}
+__constant__ BorderTab kBorderTab = make_bordertab();
+
 
 // ---------------------------------------------------------------------------------------------
 // small helpers
@@ -405,6 +428,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 	const Vp8gFrameDesc& D = descs[f];
 
 	for (int i = (int)threadIdx.x; i < kBpModes * 32; i += NW * 64) ((uint32_t*)(smem + kBpTable))[i] = kBpTab.v[i];
+	if (threadIdx.x < 32) ((uint32_t*)(smem + kBorderTable))[threadIdx.x] = kBorderTab.v[threadIdx.x];
 	if (threadIdx.x < 24) ((int16_t*)(smem + kDqTable))[threadIdx.x] = D.dq[threadIdx.x / 6][threadIdx.x % 6];
 	if (threadIdx.x < 32) smem[kLfTable + threadIdx.x] = D.lf[threadIdx.x >> 3][(threadIdx.x >> 2) & 1][threadIdx.x & 3];
 	if (threadIdx.x < 16) ((uint32_t*)(smem + kProgress))[threadIdx.x] = 0;
@@ -623,23 +647,20 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 						st64(tC + p * 16 + (4 + row) * kTP + slot * 8, u32x2{ld32(s), ld32(s + 4)});
 					}
 				} else {
-					// ln 0..3 luma above row, 4 luma above-right (cols x+16..x+19, clamped to the
-					// padded width in the last column), 5..8 chroma above rows; 9..16 left columns at
-					// the frame's left edge (129); 17..19 corners there (127 on the top row, else 129);
-					// 20..31 the filter state of the MB above (luma 4 x 16 B, chroma 8 x 8 B).
-					const bool ar = ln == 4;
-					const bool clampc = ar && cu + 1 == C;
-					const int q = ln - 5;
-					const uint32_t soff = ln < 4 ? rec_off(cu) + 4 * ln
-					                             : (ar ? (clampc ? rec_off(cu) + 12 : rec_off(cu + 1))
-					                                   : rec_off(cu) + 16 + 8 * (q >> 1) + 4 * (q & 1));
-					uint8_t* const dst32 = ln < 4 ? abY + 16 + 4 * ln
-					                              : (ar ? abY + 32 : (ln < 9 ? abUV + 8 + 16 * (q >> 1) + 4 * (q & 1) : left + 4 * (ln - 9)));
-					uint32_t v = 0x81818181u;
-					if (ln < 9) v = top ? 0x7F7F7F7Fu : ctx.rd(soff);
-					if (clampc && !top) v = (v >> 24) * 0x01010101u;
-					if (ln < 9 || (ln < 17 && c == 0)) st32(dst32, v);
-					if (ln >= 17 && ln < 20 && c == 0) (ln == 17 ? abY + 15 : abUV + 7 + 16 * (ln - 18))[0] = top ? 127 : 129;
+					// One 4-byte store per lane 0..19 (kBorderTab: destination, context source, kind):
+					// ln 0..3 luma above row, 4 luma above-right (cols x+16..x+19; in the last column
+					// the padded width's last byte, replicated), 5..8 chroma above rows -- 127 on the
+					// top row; 9..16 left columns at the frame's left edge (129); 17..19 the corners
+					// there (byte 3 of the word: 127 on the top row, else 129).
+					const uint32_t bt = ((const uint32_t*)(smem + kBorderTable))[ln];
+					const bool clampc = ln == 4 && cu + 1 == C;
+					const uint32_t rsrc = rec_off(cu + ((ln == 4 && !clampc) ? 1u : 0u)) + (clampc ? 12u : ((bt >> 12) & 0xFFu));
+					const uint32_t ldv = ctx.rd(rsrc);
+					const uint32_t kind = bt >> 20;
+					const uint32_t vabove = top ? 0x7F7F7F7Fu : (clampc ? __builtin_amdgcn_perm(ldv, ldv, 0x03030303u) : ldv);
+					const uint32_t vcorner = top ? 0x7F000000u : 0x81000000u;
+					const uint32_t v = kind == 0 ? vabove : (kind == 1 ? 0x81818181u : vcorner);
+					if (ln < 20 && (kind == 0 || c == 0)) st32(hv + (bt & 0xFFFu), v);
 				}
 				if (lf_on && !top && ln >= 20) {  // filter state of the MB above (both modes)
 					const bool ly = ln < 24;
