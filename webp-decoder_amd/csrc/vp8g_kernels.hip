@@ -186,6 +186,12 @@ DEV uint32_t as_w(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
 DEV uint32_t pk_add(uint32_t a, uint32_t b) { return as_w(as_p(a) + as_p(b)); }
 DEV uint32_t pk_sub(uint32_t a, uint32_t b) { return as_w(as_p(a) - as_p(b)); }
 DEV uint32_t pk_mul(uint32_t a, uint32_t b) { return as_w(as_p(a) * as_p(b)); }
+typedef int16_t s16x2 __attribute__((ext_vector_type(2)));
+DEV uint32_t pk_clamp255(uint32_t x) {  // each int16 half clamped to [0, 255] (v_pk_max_i16 + v_pk_min_i16)
+	s16x2 v = __builtin_bit_cast(s16x2, x);
+	v = __builtin_elementwise_min(__builtin_elementwise_max(v, s16x2{0, 0}), s16x2{255, 255});
+	return __builtin_bit_cast(uint32_t, v);
+}
 DEV int lo_s16(uint32_t x) { return (int)(int16_t)(x & 0xFFFFu); }
 DEV int hi_s16(uint32_t x) { return (int)(int16_t)(x >> 16); }
 DEV uint32_t pack2(int a, int b) { return __builtin_amdgcn_perm((uint32_t)b, (uint32_t)a, 0x05040100u); }
@@ -699,26 +705,23 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					const uint32_t aw = ld32(ab + 4 * bx);
 					const uint32_t lw = ld32(lc + 4 * by);
 					const int P = (int)ab[-1];
-					const uint32_t mA = (mode == 1 || mode == 3) ? 0xFFu : 0u;
-					const uint32_t mL = (mode == 2 || mode == 3) ? 0xFFu : 0u;
+					// two pixels per op as int16 pairs (|residual| < 2^14, so nothing wraps)
+					const uint32_t mA = (mode == 1 || mode == 3) ? 0x00FF00FFu : 0u;
+					const uint32_t mL = (mode == 2 || mode == 3) ? 0x00FF00FFu : 0u;
 					const int K = (mode == 3 ? -P : 0) + (mode == 0 ? dcv : 0);
+					const uint32_t K2 = __builtin_amdgcn_perm((uint32_t)K, (uint32_t)K, 0x05040100u);  // K in both halves
 					uint8_t* dst = yl ? tY + (4 + 4 * by) * kTP + slot * 16 + 4 * bx
 					                  : tC + p * 16 + (4 + 4 * by) * kTP + slot * 8 + 4 * bx;
 					const u32x4 r01 = ld128(hv + kResid + ln * 32), r23 = ld128(hv + kResid + ln * 32 + 16);
 					const uint32_t rw[8] = {r01.x, r01.y, r01.z, r01.w, r23.x, r23.y, r23.z, r23.w};
-					int acol[4];
-#pragma unroll
-					for (int cc = 0; cc < 4; cc++) acol[cc] = (int)((aw >> (8 * cc)) & mA) + K;
+					const uint32_t A01 = pk_add(__builtin_amdgcn_perm(aw, aw, 0x0C010C00u) & mA, K2);
+					const uint32_t A23 = pk_add(__builtin_amdgcn_perm(aw, aw, 0x0C030C02u) & mA, K2);
 #pragma unroll
 					for (int rr = 0; rr < 4; rr++) {
-						const int L = (int)((lw >> (8 * rr)) & mL);
-						int px4[4];
-#pragma unroll
-						for (int cc = 0; cc < 4; cc++) {
-							const int rv = (int)(int16_t)((rw[(4 * rr + cc) >> 1] >> (16 * (cc & 1))) & 0xFFFFu);
-							px4[cc] = sat8(sat8(L + acol[cc]) + rv);
-						}
-						st32(dst + rr * kTP, pack4(px4[0], px4[1], px4[2], px4[3]));
+						const uint32_t L2 = __builtin_amdgcn_perm(lw, lw, 0x0C000C00u + 0x00010001u * rr) & mL;
+						const uint32_t p01 = pk_clamp255(pk_add(pk_clamp255(pk_add(L2, A01)), rw[2 * rr]));
+						const uint32_t p23 = pk_clamp255(pk_add(pk_clamp255(pk_add(L2, A23)), rw[2 * rr + 1]));
+						st32(dst + rr * kTP, __builtin_amdgcn_perm(p23, p01, 0x06040200u));
 					}
 				}
 				wave_lds_sync();
