@@ -467,34 +467,19 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 #endif
 
 	// Loads for one lane of one step: coefficient blocks (ln 0..24), bmode (25), side bytes (26..29).
-	// Straight-line: every lane issues the same three loads; lanes without a role (and halves
-	// outside the frame, which read MB mb0) load duplicate addresses and ignore the result.
-	auto prefetch = [&](int lane, uint32_t rA, bool two, int tt) -> Pref {
+	// Straight-line: every lane issues the same three loads from a per-pair row base (hoisted, see
+	// below) plus its column; columns outside the frame are clamped (their data is never used).
+	// Loop-filter-only frames read the descriptor instead of the absent coefficient arrays: a
+	// path without these loads would make the compiler's wait-count analysis fall back to
+	// vmcnt(0) on the next step's use of the side bytes, i.e. wait for this very prefetch.
+	auto prefetch = [&](int lane, uint64_t cbase, uint64_t sbase, uint32_t csh, int tt) -> Pref {
 		Pref p;
 		const int hh = lane >> 5, ln = lane & 31;
-		const int cn = tt - 2 * hh;
-		const bool inb = (hh == 0 || two) && cn >= 0 && cn < (int)C;
-		const uint64_t m = mb0 + (inb ? (uint64_t)(__umul24(rA + hh, C) + (uint32_t)cn) : 0ull);
-		// Issued unconditionally (loop-filter-only frames read the descriptor instead of the
-		// absent coefficient arrays): a path without these loads would make the compiler's
-		// wait-count analysis fall back to vmcnt(0) on the next step's use of the side bytes,
-		// i.e. wait for this very prefetch.
-		{
-			const bool isb = ln == 25;
-			const uint64_t idx = ln < 16 ? m * 16 + ln : (ln < 24 ? m * 4 + (ln & 3) : m);
-			// (vsel: explicit v_cndmask -- a select among struct fields by a lane-dependent index
-			// would otherwise compile to a per-lane load from the kernel-argument block)
-			const uint64_t base = vsel(ln < 16, (uint64_t)A.coeff_y,
-			                           vsel(ln < 20, (uint64_t)A.coeff_u, vsel(ln < 24, (uint64_t)A.coeff_v, (uint64_t)A.coeff_y2)));
-			const uint64_t addr = vsel(isb, (uint64_t)A.bmode + m * 16, base + idx * 32);
-			const gu32x4* src = (const gu32x4*)(lf_only ? (uint64_t)descs : addr);
-			p.a = __builtin_nontemporal_load(src);
-			p.b = __builtin_nontemporal_load(isb ? src : src + 1);
-		}
-		const int q = ln & 3;  // lanes 26..29: ymode, uv_mode, segment_id, has_coeff
-		const uint8_t* sp = (const uint8_t*)vsel(q == 2, (uint64_t)A.ymode,
-		                                         vsel(q == 3, (uint64_t)A.uv_mode, vsel(q == 0, (uint64_t)A.segment_id, (uint64_t)A.has_coeff)));
-		p.side = ((const __attribute__((address_space(1))) uint8_t*)sp)[m];
+		const uint32_t cn = (uint32_t)min(max(tt - 2 * hh, 0), (int)C - 1);
+		const gu32x4* src = (const gu32x4*)(cbase + ((uint64_t)cn << csh));
+		p.a = __builtin_nontemporal_load(src);
+		p.b = __builtin_nontemporal_load(ln == 25 ? src : src + 1);
+		p.side = ((const __attribute__((address_space(1))) uint8_t*)sbase)[cn];
 		return p;
 	};
 
@@ -502,7 +487,29 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 		const uint32_t rA = 2 * k;
 		const bool two = rA + 1 < R;
 		const uint32_t T = two ? CP2 : C;
-		Pref nxt = prefetch(lane0, rA, two, 0);
+		// Per-lane row bases of this pair (lane roles: ln 0..24 one 32-B coefficient block each --
+		// Y 0..15, U 16..19, V 20..23, Y2 24 (and 26..31, duplicates) -- ln 25 the 16 B_PRED modes;
+		// side bytes ln&3: ymode, uv_mode, segment_id, has_coeff for lanes 26..29).  MB m's data
+		// sits at cbase + (column << csh).
+		uint64_t cbase, sbase;
+		uint32_t csh;
+		{
+			const int hh = lane0 >> 5, ln = lane0 & 31;
+			const uint64_t mrow = mb0 + __umul24(rA + (two ? (uint32_t)hh : 0u), C);
+			const bool isb = ln == 25;
+			const uint32_t sh = ln < 16 ? 9u : (ln < 24 ? 7u : (isb ? 4u : 5u));
+			const uint32_t boff = ln < 16 ? (uint32_t)ln * 32u : (ln < 24 ? (uint32_t)(ln & 3) * 32u : 0u);
+			// (vsel: explicit v_cndmask -- a select among struct fields by a lane-dependent index
+			// would otherwise compile to a per-lane load from the kernel-argument block)
+			const uint64_t base = vsel(ln < 16, (uint64_t)A.coeff_y,
+			                           vsel(ln < 20, (uint64_t)A.coeff_u,
+			                                vsel(ln < 24, (uint64_t)A.coeff_v, vsel(isb, (uint64_t)A.bmode, (uint64_t)A.coeff_y2))));
+			cbase = lf_only ? (uint64_t)descs : base + (mrow << sh) + boff;
+			csh = lf_only ? 0u : sh;
+			const int q = ln & 3;
+			sbase = vsel(q == 2, (uint64_t)A.ymode, vsel(q == 3, (uint64_t)A.uv_mode, vsel(q == 0, (uint64_t)A.segment_id, (uint64_t)A.has_coeff))) + mrow;
+		}
+		Pref nxt = prefetch(lane0, cbase, sbase, csh, 0);
 
 		for (uint32_t t = 0; t < T; t++) {
 			// Lane-derived values are recomputed every step from a laundered lane id: hoisting the
@@ -523,7 +530,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			uint8_t* const left = hv + kLeft;
 
 			const Pref cur = nxt;
-			nxt = prefetch(lane, rA, two, (int)t + 1);
+			nxt = prefetch(lane, cbase, sbase, csh, (int)t + 1);
 
 			// per-half side info (lanes 26..29 / 58..61 hold it)
 			const int sd26 = rdlane((int)cur.side, 26), sd27 = rdlane((int)cur.side, 27), sd28 = rdlane((int)cur.side, 28),
