@@ -144,8 +144,8 @@ constexpr BorderTab make_bordertab() {
 			const int q = ln - 5;
 			t.v[ln] = BE(kAbUV + 8 + 16 * (q >> 1) + 4 * (q & 1), 16 + 8 * (q >> 1) + 4 * (q & 1), 0);
 		} else if (ln < 17) t.v[ln] = BE(kLeft + 4 * (ln - 9), 0, 1);
-		else if (ln == 17) t.v[ln] = BE(kAbY + 12, 0, 2);
-		else if (ln < 20) t.v[ln] = BE(kAbUV + 4 + 16 * (ln - 18), 0, 2);
+		else if (ln == 17) t.v[ln] = BE(kAbY + 12, 19, 2);  // corner P from the old abY[31]
+		else if (ln < 20) t.v[ln] = BE(kAbUV + 4 + 16 * (ln - 18), 11, 2);  // from abUV[15] / abUV[31]
 		else t.v[ln] = BE(0, 0, 3);
 	}
 	return t;
@@ -231,6 +231,14 @@ struct Ctx {
 	DEV u32x4 rd128(uint32_t off) const {
 		if constexpr (kG) return u32x4{rd(off), rd(off + 4), rd(off + 8), rd(off + 12)};
 		else return ld128(lds + off);
+	}
+	DEV void wr8(uint32_t off, uint32_t v) const {
+		if constexpr (kG) g[off] = (uint8_t)v;
+		else lds[off] = (uint8_t)v;
+	}
+	DEV void wr32(uint32_t off, uint32_t v) const {
+		if constexpr (kG) *(uint32_t*)(g + off) = v;
+		else st32(lds + off, v);
 	}
 	DEV void wr64(uint32_t off, u32x2 v) const {
 		if constexpr (kG) *(u32x2*)(g + off) = v;
@@ -671,9 +679,12 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					const uint32_t ldv = ctx.rd(rsrc);
 					const uint32_t kind = bt >> 20;
 					const uint32_t vabove = top ? 0x7F7F7F7Fu : (clampc ? __builtin_amdgcn_perm(ldv, ldv, 0x03030303u) : ldv);
-					const uint32_t vcorner = top ? 0x7F000000u : 0x81000000u;
+					// corner: at the left edge a constant, else the previous MB's above row's last byte
+					// (still in the above-row buffer: read before this step's stores replace it)
+					const uint32_t oldb = hv[(bt & 0xFFFu) + ((bt >> 12) & 0xFFu)];
+					const uint32_t vcorner = c == 0 ? (top ? 0x7F000000u : 0x81000000u) : oldb << 24;
 					const uint32_t v = kind == 0 ? vabove : (kind == 1 ? 0x81818181u : vcorner);
-					if (ln < 20 && (kind == 0 || c == 0)) st32(hv + (bt & 0xFFFu), v);
+					if (ln < 20 && (kind != 1 || c == 0)) st32(hv + (bt & 0xFFFu), v);
 				}
 				if (lf_on && !top && ln >= 20) {  // filter state of the MB above (both modes)
 					const bool ly = ln < 24;
@@ -723,12 +734,23 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					const uint32_t rw[8] = {r01.x, r01.y, r01.z, r01.w, r23.x, r23.y, r23.z, r23.w};
 					const uint32_t A01 = pk_add(__builtin_amdgcn_perm(aw, aw, 0x0C010C00u) & mA, K2);
 					const uint32_t A23 = pk_add(__builtin_amdgcn_perm(aw, aw, 0x0C030C02u) & mA, K2);
+					uint32_t wv[4];
 #pragma unroll
 					for (int rr = 0; rr < 4; rr++) {
 						const uint32_t L2 = __builtin_amdgcn_perm(lw, lw, 0x0C000C00u + 0x00010001u * rr) & mL;
 						const uint32_t p01 = pk_clamp255(pk_add(pk_clamp255(pk_add(L2, A01)), rw[2 * rr]));
 						const uint32_t p23 = pk_clamp255(pk_add(pk_clamp255(pk_add(L2, A23)), rw[2 * rr + 1]));
-						st32(dst + rr * kTP, __builtin_amdgcn_perm(p23, p01, 0x06040200u));
+						wv[rr] = __builtin_amdgcn_perm(p23, p01, 0x06040200u);
+						st32(dst + rr * kTP, wv[rr]);
+					}
+					// the MB's unfiltered bottom row -> ctx_rec[c] (the next MB row's above row) and its
+					// right column -> the left column of the next MB (reference vp8_recon.c:395-421)
+					const int last = yl ? 3 : 1;
+					if (by == last) ctx.wr32(rec_off(cu) + (yl ? 4 * bx : 16 + 8 * p + 4 * bx), wv[3]);
+					if (bx == last) {
+						const uint32_t c01 = __builtin_amdgcn_perm(wv[1], wv[0], 0x0C0C0703u);
+						const uint32_t c23 = __builtin_amdgcn_perm(wv[3], wv[2], 0x0C0C0703u);
+						st32((yl ? left : left + 16 + 8 * p) + 4 * by, __builtin_amdgcn_perm(c23, c01, 0x05040100u));
 					}
 				}
 				wave_lds_sync();
@@ -788,9 +810,11 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 							const int pred = mode == 0 ? vdc : (mode == 1 ? vtm : vt);
 							const int px = sat8(pred + rv);
 							tpix[kBS * i0 + 4 * s] = (uint8_t)px;
-							// right pixel column of a sub-block: left column of the next sub-block column
-							const bool w3 = (g ? j0 - 2 : j0) < 3;
-							if (col3 && w3) lb[-16 + rr] = (uint8_t)px;
+							// right pixel column of a sub-block: left column of the next sub-block column (in
+							// sub-block column 3: of the next MB); the MB's bottom row -> ctx_rec[c]
+							const bool j3 = g ? j0 == 5 : j0 == 3;
+							if (col3) (j3 ? left + 4 * (i0 + g) + rr : lb - 16 + rr)[0] = (uint8_t)px;
+							if (i0 + g == 3 && rr == 3) ctx.wr8(rec_off(cu) + 4 * (g ? j0 - 2 : j0) + cc, (uint32_t)px);
 						}
 						wave_lds_sync();
 					}
@@ -799,26 +823,8 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			wave_lds_sync();
 			STAMP(3);
 
-			// ---------------------------------------------- save unfiltered context
-			if (act && !lf_only) {
-				// right column -> left column of the next MB (Y 16, U 8, V 8 lanes)
-				const uint8_t* sp = ln < 16 ? tY + (4 + ln) * kTP + slot * 16 + 15
-				                            : tC + ((ln >> 3) & 1) * 16 + (4 + (ln & 7)) * kTP + slot * 8 + 7;
-				const uint8_t pxv = *sp;
-				if (ln == 0) {  // bottom rows -> ctx_rec[c]
-					ctx.wr64(rec_off(cu), ld64(tY + 19 * kTP + slot * 16));
-					ctx.wr64(rec_off(cu) + 8, ld64(tY + 19 * kTP + slot * 16 + 8));
-				}
-				else if (ln == 1) ctx.wr64(rec_off(cu) + 16, ld64(tC + 11 * kTP + slot * 8));
-				else if (ln == 2) ctx.wr64(rec_off(cu) + 24, ld64(tC + 16 + 11 * kTP + slot * 8));
-				else if (ln == 3) {  // corner for the next MB
-					abY[15] = abY[31];
-					abUV[7] = abUV[15];
-					abUV[23] = abUV[31];
-				}
-				left[ln] = pxv;
-			}
-			wave_lds_sync();
+			// (the unfiltered bottom row / right column were saved by the prediction lanes; the
+			// corner for the next MB is taken at its border setup)
 			STAMP(4);
 
 			// ---------------------------------------------- loop filter MB(r, c)
