@@ -20,9 +20,9 @@ constexpr int kAbUV = 1328;   // chroma above rows: U P@7 A@8..15, V P@23 A@24..
 constexpr int kColY = 1360;   // B_PRED: luma columns 11, 7, 3 of the MB (16 B each, in that order),
                               // so that the left column of sub-block column j is at kLeft - 16 j
 constexpr int kLeft = 1408;   // unfiltered left columns: Y 0..15, U 16..23, V 24..31
-constexpr int kResid = 1440;  // residual of the MB: 25 blocks (16 Y, 4 U, 4 V, Y2 slot) x 16 int16
-constexpr int kWht = 2240;    // 16 int16 luma DCs out of the inverse WHT
-constexpr int kHalfBytes = 2272;
+constexpr int kResid = 1440;  // luma residual of the MB (for B_PRED): 16 blocks x 16 int16
+constexpr int kWht = 1952;    // 16 int16 luma DCs out of the inverse WHT
+constexpr int kHalfBytes = 1984;
 constexpr int kWaveBytes = 2 * kHalfBytes;
 
 // Workgroup header.

@@ -552,9 +552,14 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			const uint32_t y0 = r * 16, cy0 = r * 8, x0 = cu * 16, cx0 = cu * 8;
 
 			// ---------------------------------------------- residual (no spatial dependency)
-			// Computed before the dependency wait and parked in LDS (kResid, 32 B per block) so that
-			// no residual registers stay live across the wait.
-			if (!lf_only) {
+			// Computed before the dependency wait.  Each block stays in its lane's registers (rs[],
+			// packed int16 pairs) for the whole-block predictors of the same lane; the luma blocks
+			// are also parked in LDS (kResid) for the B_PRED pixel lanes.
+			uint32_t rs[8];
+			if (lf_only) {
+#pragma unroll
+				for (int i = 0; i < 8; i++) rs[i] = 0u;
+			} else {
 				// Packed int16 pairs: w[2r + h] = row r, columns 2h, 2h+1.  Dequantisation and the
 				// vertical pass wrap mod 2^16 exactly like the reference's int16 stores; the
 				// horizontal pass (whose (x + 4) >> 3 needs the full-precision sum) runs in 32 bits.
@@ -596,7 +601,6 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 				}
 				// inverse DCT (RFC 14.4), whole 4x4 block per lane; DC-only shortcut when no lane
 				// of the wave has an AC coefficient ((dc+4)>>3 everywhere, exact)
-				uint32_t rs[8];
 				if (__ballot(anyac && ln < 24 && act) != 0ull) {
 					uint32_t o[8];
 #pragma unroll
@@ -622,7 +626,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 #pragma unroll
 					for (int i = 0; i < 8; i++) rs[i] = pack2(d, d);
 				}
-				if (ln < 24) {
+				if (ln < 16) {
 					uint8_t* rp = hv + kResid + ln * 32;
 					st128(rp, u32x4{rs[0], rs[1], rs[2], rs[3]});
 					st128(rp + 16, u32x4{rs[4], rs[5], rs[6], rs[7]});
@@ -730,8 +734,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					const uint32_t K2 = __builtin_amdgcn_perm((uint32_t)K, (uint32_t)K, 0x05040100u);  // K in both halves
 					uint8_t* dst = yl ? tY + (4 + 4 * by) * kTP + slot * 16 + 4 * bx
 					                  : tC + p * 16 + (4 + 4 * by) * kTP + slot * 8 + 4 * bx;
-					const u32x4 r01 = ld128(hv + kResid + ln * 32), r23 = ld128(hv + kResid + ln * 32 + 16);
-					const uint32_t rw[8] = {r01.x, r01.y, r01.z, r01.w, r23.x, r23.y, r23.z, r23.w};
+					const uint32_t* const rw = rs;  // this lane's own block
 					const uint32_t A01 = pk_add(__builtin_amdgcn_perm(aw, aw, 0x0C010C00u) & mA, K2);
 					const uint32_t A23 = pk_add(__builtin_amdgcn_perm(aw, aw, 0x0C030C02u) & mA, K2);
 					uint32_t wv[4];
