@@ -485,8 +485,10 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 		const int hh = lane >> 5, ln = lane & 31;
 		const uint32_t cn = (uint32_t)min(max(tt - 2 * hh, 0), (int)C - 1);
 		const gu32x4* src = (const gu32x4*)(cbase + ((uint64_t)cn << csh));
-		p.a = __builtin_nontemporal_load(src);
-		p.b = __builtin_nontemporal_load(ln == 25 ? src : src + 1);
+		// (default cache policy: non-temporal loads measured 1 % slower and cost 11 % more HBM
+		// writes -- streamed coefficients then crowd out the partially written output lines in L2)
+		p.a = *src;
+		p.b = *(ln == 25 ? src : src + 1);
 		p.side = ((const __attribute__((address_space(1))) uint8_t*)sbase)[cn];
 		return p;
 	};
