@@ -519,6 +519,24 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			const int q = ln & 3;
 			sbase = vsel(q == 2, (uint64_t)A.ymode, vsel(q == 3, (uint64_t)A.uv_mode, vsel(q == 0, (uint64_t)A.segment_id, (uint64_t)A.has_coeff))) + mrow;
 		}
+		// Per-lane flush geometry of this pair (loop-filtered frames): lane ln of a half stores
+		// luma tile row ln (0..19) and chroma plane ln / 12, tile row ln % 12 of some column;
+		// image row = MB row origin + tile row - 4 (negative rows wrap and fail the crop test).
+		uint32_t fl_offY, fl_offC, fl_bits;
+		{
+			const int hh = lane0 >> 5, ln = lane0 & 31;
+			const uint32_t rr = rA + (uint32_t)hh;
+			const bool row_ok = hh == 0 || two;
+			const uint32_t prowY = rr * 16u + (uint32_t)ln - 4u;
+			const int pc = ln >= 12 ? 1 : 0, kc = ln - 12 * pc;
+			const uint32_t prowC = rr * 8u + (uint32_t)kc - 4u;
+			fl_offY = __umul24(prowY, sy);
+			fl_offC = (pc ? vofs : 0u) + __umul24(prowC, suv);
+			const bool nlast = rr + 1 < R;
+			fl_bits = (row_ok && ln < 20 && prowY < H ? 1u : 0u) | (ln >= 16 && nlast ? 2u : 0u) |
+			          (((yal + fl_offY) & 15u) == 0 ? 4u : 0u) | (row_ok && ln < 24 && prowC < CH ? 8u : 0u) |
+			          (kc >= 8 && nlast ? 16u : 0u) | (((ual + fl_offC) & 7u) == 0 ? 32u : 0u);
+		}
 		Pref nxt = prefetch(lane0, cbase, sbase, csh, 0);
 
 		for (uint32_t t = 0; t < T; t++) {
@@ -910,12 +928,42 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 				};
 				{  // luma: ln 0..3 the MB above's bottom rows (this column, final now); 4..19 the left MB
 					const bool top = ln < 4;
-					flushY(act && ln < 20 && (top ? r > 0 : c > 0), ln, top ? cu : cu - 1, top ? slot : slot ^ 1);
+					const uint32_t col = top ? cu : cu - 1;
+					const uint8_t* src = tY + ln * kTP + (top ? slot : slot ^ 1) * 16;
+					const u32x2 lo = ld64(src), hi = ld64(src + 8);
+					const bool ok = act && (fl_bits & 1u) && (top || c > 0);
+					const bool to_ctx = ok && (fl_bits & 2u);
+					if (to_ctx) ctx.wr128(lf_off(col) + (ln - 16) * 16, u32x4{lo.x, lo.y, hi.x, hi.y});
+					const uint32_t colpx = col * 16u, off = fl_offY + colpx;
+					const bool vis = ok && !to_ctx && !(VP8G_ABLATE & 4);
+					const bool full = (fl_bits & 4u) && colpx + 16u <= W;
+					if (vis && full) *(u32x4*)(outY + off) = u32x4{lo.x, lo.y, hi.x, hi.y};
+					if (__ballot(vis && !full) != 0ull) {
+						if (vis && !full) {
+							const uint32_t n = W - colpx, cnt = n < 16u ? n : 16u;
+							for (uint32_t q = 0; q < cnt; q++) outY[off + q] = src[q];
+						}
+					}
 				}
 				{  // chroma: plane ln / 12, tile row ln % 12 (same split)
 					const int p = ln >= 12 ? 1 : 0, k = ln - 12 * p;
 					const bool top = k < 4;
-					flushC(act && ln < 24 && (top ? r > 0 : c > 0), p, k, top ? cu : cu - 1, top ? slot : slot ^ 1);
+					const uint32_t col = top ? cu : cu - 1;
+					const uint8_t* src = tC + p * 16 + k * kTP + (top ? slot : slot ^ 1) * 8;
+					const u32x2 lo = ld64(src);
+					const bool ok = act && (fl_bits & 8u) && (top || c > 0);
+					const bool to_ctx = ok && (fl_bits & 16u);
+					if (to_ctx) ctx.wr64(lf_off(col) + 64 + p * 32 + (k - 8) * 8, lo);
+					const uint32_t colpx = col * 8u, off = fl_offC + colpx;
+					const bool vis = ok && !to_ctx && !(VP8G_ABLATE & 4);
+					const bool full = (fl_bits & 32u) && colpx + 8u <= CW;
+					if (vis && full) *(u32x2*)(outU + off) = lo;
+					if (__ballot(vis && !full) != 0ull) {
+						if (vis && !full) {
+							const uint32_t n = CW - colpx, cnt = n < 8u ? n : 8u;
+							for (uint32_t q = 0; q < cnt; q++) outU[off + q] = src[q];
+						}
+					}
 				}
 				SUBMARK(21);
 				if (__ballot(act && cu + 1 == C) != 0ull) {  // last column: its own rows are final too
