@@ -31,8 +31,7 @@ constexpr int kBpTable = 64;      // B_PRED predictor table: 11 modes x 16 px x 
 constexpr int kBpModes = 11;      // modes 0..9 + one constant-128 entry for out-of-range modes
 constexpr int kDqTable = kBpTable + kBpModes * 16 * 8;  // 4 segments x 6 int16 dequant factors
 constexpr int kLfTable = kDqTable + 48;                 // 4 segments x 2 (B_PRED?) x {E, I, T, 0}
-constexpr int kBorderTable = kLfTable + 32;            // 32 lanes x u32 border-setup roles
-constexpr int kHdrBytes = kBorderTable + 128;
+constexpr int kHdrBytes = kLfTable + 32;
 
 // Shared per-MB-column context (one frame per workgroup).
 constexpr int kCtxRecBytes = 32;   // unfiltered bottom row: Y 16, U 8, V 8 (intra prediction)

@@ -442,7 +442,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 	const Vp8gFrameDesc& D = descs[f];
 
 	for (int i = (int)threadIdx.x; i < kBpModes * 32; i += NW * 64) ((uint32_t*)(smem + kBpTable))[i] = kBpTab.v[i];
-	if (threadIdx.x < 32) ((uint32_t*)(smem + kBorderTable))[threadIdx.x] = kBorderTab.v[threadIdx.x];
+	const uint32_t bt_lane = kBorderTab.v[lane0 & 31];  // this lane's border-setup role (loop-invariant)
 	if (threadIdx.x < 24) ((int16_t*)(smem + kDqTable))[threadIdx.x] = D.dq[threadIdx.x / 6][threadIdx.x % 6];
 	if (threadIdx.x < 32) smem[kLfTable + threadIdx.x] = D.lf[threadIdx.x >> 3][(threadIdx.x >> 2) & 1][threadIdx.x & 3];
 	if (threadIdx.x < 16) ((uint32_t*)(smem + kProgress))[threadIdx.x] = 0;
@@ -697,7 +697,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					// the padded width's last byte, replicated), 5..8 chroma above rows -- 127 on the
 					// top row; 9..16 left columns at the frame's left edge (129); 17..19 the corners
 					// there (byte 3 of the word: 127 on the top row, else 129).
-					const uint32_t bt = ((const uint32_t*)(smem + kBorderTable))[ln];
+					const uint32_t bt = bt_lane;
 					const bool clampc = ln == 4 && cu + 1 == C;
 					const uint32_t rsrc = rec_off(cu + ((ln == 4 && !clampc) ? 1u : 0u)) + (clampc ? 12u : ((bt >> 12) & 0xFFu));
 					const uint32_t ldv = ctx.rd(rsrc);
