@@ -561,13 +561,13 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			nxt = prefetch(lane, cbase, sbase, csh, (int)t + 1);
 
 			// per-half side info (lanes 26..29 / 58..61 hold it)
-			const int sd26 = rdlane((int)cur.side, 26), sd27 = rdlane((int)cur.side, 27), sd28 = rdlane((int)cur.side, 28),
-			          sd29 = rdlane((int)cur.side, 29), sd58 = rdlane((int)cur.side, 58), sd59 = rdlane((int)cur.side, 59),
-			          sd60 = rdlane((int)cur.side, 60), sd61 = rdlane((int)cur.side, 61);
-			const int ymode = hh ? sd58 : sd26;
-			const int uvmode = hh ? sd59 : sd27;
-			const int seg = (hh ? sd60 : sd28) & 3;
-			const int hasc = hh ? sd61 : sd29;
+			// per-half side info, held by lanes 26..29 / 58..61: fetched with ds_bpermute (LDS
+			// crossbar, no LDS memory) instead of readlane + per-half select
+			const int sdl = (hh ? 58 : 26) * 4;
+			const int ymode = __builtin_amdgcn_ds_bpermute(sdl, (int)cur.side);
+			const int uvmode = __builtin_amdgcn_ds_bpermute(sdl + 4, (int)cur.side);
+			const int seg = __builtin_amdgcn_ds_bpermute(sdl + 8, (int)cur.side) & 3;
+			const int hasc = __builtin_amdgcn_ds_bpermute(sdl + 12, (int)cur.side);
 			const bool bpred = ymode == 4;
 			const uint32_t y0 = r * 16, cy0 = r * 8, x0 = cu * 16, cx0 = cu * 8;
 
@@ -789,11 +789,11 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					// last sub-block column come from the MB above (abY + 32), the left column of
 					// sub-block column j is at kLeft - 16 j (kColY, written here by the lanes of
 					// pixel column 3), P is the byte before the above row (i == 0) or the left column.
-					const u32x4 bm0 = u32x4{(uint32_t)rdlane((int)cur.a.x, 25), (uint32_t)rdlane((int)cur.a.y, 25),
-					                        (uint32_t)rdlane((int)cur.a.z, 25), (uint32_t)rdlane((int)cur.a.w, 25)};
-					const u32x4 bm1 = u32x4{(uint32_t)rdlane((int)cur.a.x, 57), (uint32_t)rdlane((int)cur.a.y, 57),
-					                        (uint32_t)rdlane((int)cur.a.z, 57), (uint32_t)rdlane((int)cur.a.w, 57)};
-					const u32x4 bmw = hh ? bm1 : bm0;
+					const int bml = (hh ? 57 : 25) * 4;  // the half's mode list, from lane 25 / 57
+					const u32x4 bmw = u32x4{(uint32_t)__builtin_amdgcn_ds_bpermute(bml, (int)cur.a.x),
+					                        (uint32_t)__builtin_amdgcn_ds_bpermute(bml, (int)cur.a.y),
+					                        (uint32_t)__builtin_amdgcn_ds_bpermute(bml, (int)cur.a.z),
+					                        (uint32_t)__builtin_amdgcn_ds_bpermute(bml, (int)cur.a.w)};
 					const int g = (ln >> 4) & 1, p = ln & 15, rr = p >> 2, cc = p & 3;
 					uint8_t* const tpix = tY + slot * 16 + 4 * kTP + kBS * g + kTP * rr + cc;  // + kBS i0 + 4 s
 					const uint8_t* const tA = tY + slot * 16 + 3 * kTP + kBS * g;             // + kBS i0 + 4 s
