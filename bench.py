@@ -195,6 +195,7 @@ def main():
     value = mp * args.steps / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
     bytes_read = batch.total_mb * vp8g.BYTES_READ_PER_MB
+    bytes_written = args.frames * vp8g.i420_size(W, H)
     achieved = bytes_read / (kern_ms * 1e-3) / 1e9
     traffic = None
     if TRAFFIC_FILE.exists():
@@ -238,7 +239,10 @@ def main():
             "kernel_ms_per_step": round(kern_ms, 3),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
-                         "algorithmic_bytes_per_launch": bytes_read},
+                         "algorithmic_bytes_per_launch": bytes_read,
+                         # SURVEY.md §8(d) secondary figure: read + written algorithmic bytes
+                         "achieved_read_write": round((bytes_read + bytes_written) / (kern_ms * 1e-3) / 1e9, 1),
+                         "binding_resource": "vector-instruction issue (VALU), see DESIGN.md §5"},
             "cpu_baseline": cpu,
         }
         if stamp_shares:
