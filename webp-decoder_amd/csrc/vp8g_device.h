@@ -27,9 +27,10 @@ constexpr int kWaveBytes = 2 * kHalfBytes;
 
 // Workgroup header.
 constexpr int kProgress = 0;      // 16 x u32 progress words (one per wave)
-constexpr int kBpTable = 64;      // B_PRED predictor table: 11 modes x 16 px x {perm selectors, byte mask}
+constexpr int kBpTable = 64;      // B_PRED predictor table: 11 modes x 16 px x {perm selectors, byte
+                                  // mask, dot weights, bias | shift}
 constexpr int kBpModes = 11;      // modes 0..9 + one constant-128 entry for out-of-range modes
-constexpr int kDqTable = kBpTable + kBpModes * 16 * 8;  // 4 segments x 6 int16 dequant factors
+constexpr int kDqTable = kBpTable + kBpModes * 16 * 16;  // 4 segments x 6 int16 dequant factors
 constexpr int kLfTable = kDqTable + 48;                 // 4 segments x 2 (B_PRED?) x {E, I, T, 0}
 constexpr int kHdrBytes = kLfTable + 32;
 

@@ -74,13 +74,14 @@ constexpr int kBS = 4 * kTP - 8;  // B_PRED: tile offset from sub-block (i, j) t
 // Every directional mode is avg3(x, y, z) = (x + 2y + z + 2) >> 2 of three edge bytes (avg2(x, y)
 // = avg3(x, y, x), a copy = avg3(x, x, x)), so an entry is just three byte positions, stored
 // as v_perm selectors (pos & 7) plus a byte mask picking the high half (pos >= 8) of E: one
-// perm pair + one bfi fetches all three, one v_dot4_u32_u8 weighs them.  TM_PRED keeps its own
-// formula sat8(L + A - P) over the entry's positions (L_r, P, A_c); DC_PRED is a direct sum.
+// perm pair + one bfi fetches all three, one signed v_dot4 over the bytes biased by -128 weighs
+// them (avg3 weights (1, 2, 1); TM_PRED = sat8(L + A - P) is the same dot with weights
+// (1, -1, 1) over the positions (L_r, P, A_c)); DC_PRED is a direct sum.
 // Entry kBpModes-1 (all positions 128) serves out-of-range modes.
 // Edge index notation of the builders: 0..3 = L3..L0, 4 = P, 5..12 = A0..A7.
 // ---------------------------------------------------------------------------------------------
 struct BpTab {
-	uint32_t v[kBpModes * 16 * 2];
+	uint32_t v[kBpModes * 16 * 4];
 };
 constexpr int epos(int e) { return e < 4 ? 3 - e : (e == 4 ? 7 : e + 3); }
 struct Tri {
@@ -122,8 +123,13 @@ constexpr BpTab make_bptab() {
 				sel |= (uint32_t)(pos[k] & 7) << (8 * k);
 				if (pos[k] >= 8) mask |= 0xFFu << (8 * k);
 			}
-			t.v[(m * 16 + p) * 2] = sel;
-			t.v[(m * 16 + p) * 2 + 1] = mask;
+			// weights (signed bytes) and bias / shift of the one dot-product formula:
+			// value = (sdot4(E_xyz - 128, w) + bias) >> sh  (avg3: (1, 2, 1), 514, 2; TM: (1, -1, 1), 128, 0)
+			const bool tm = m == 1;
+			t.v[(m * 16 + p) * 4] = sel;
+			t.v[(m * 16 + p) * 4 + 1] = mask;
+			t.v[(m * 16 + p) * 4 + 2] = tm ? 0x0001FF01u : 0x00010201u;
+			t.v[(m * 16 + p) * 4 + 3] = tm ? 128u : (514u | (2u << 16));
 		}
 	return t;
 }
@@ -441,7 +447,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 	const uint32_t f = blockIdx.x;
 	const Vp8gFrameDesc& D = descs[f];
 
-	for (int i = (int)threadIdx.x; i < kBpModes * 32; i += NW * 64) ((uint32_t*)(smem + kBpTable))[i] = kBpTab.v[i];
+	for (int i = (int)threadIdx.x; i < kBpModes * 64; i += NW * 64) ((uint32_t*)(smem + kBpTable))[i] = kBpTab.v[i];
 	const uint32_t bt_lane = kBorderTab.v[lane0 & 31];  // this lane's border-setup role (loop-invariant)
 	if (threadIdx.x < 24) ((int16_t*)(smem + kDqTable))[threadIdx.x] = D.dq[threadIdx.x / 6][threadIdx.x % 6];
 	if (threadIdx.x < 32) smem[kLfTable + threadIdx.x] = D.lf[threadIdx.x >> 3][(threadIdx.x >> 2) & 1][threadIdx.x & 3];
@@ -800,7 +806,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					const uint8_t* const aE = g ? tA : abY + 16;                              // i0 == 0: + 4 s
 					uint8_t* const lB = left + 36 * g;                                        // + 36 i0 - 16 s
 					const int16_t* const rsp = (const int16_t*)(hv + kResid) + p + 32 * g;    // + 16 b0
-					const u32x2* const tabp = (const u32x2*)(smem + kBpTable) + p;            // + 16 mode
+					const u32x4* const tabp = (const u32x4*)(smem + kBpTable) + p;            // + 16 mode
 					const bool col3 = cc == 3;
 #pragma unroll
 					for (int s = 0; s < 10; s++) {
@@ -821,16 +827,17 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 							const uint8_t* const pp = i0 == 0 ? (g ? lb - 1 : arow - 1) : lb - 1;
 							const uint32_t a03 = ld32(arow), a47 = ld32(a47p), lw = ld32(lb);
 							const uint32_t pv = *pp;
-							const u32x2 tb = tabp[16 * mode];
+							const u32x4 tb = tabp[16 * mode];
 							const int rv = rsp[16 * b0];
 							const uint32_t ey = (pv << 24) | 0x808080u;
 							const uint32_t lo = __builtin_amdgcn_perm(ey, lw, tb.x);
 							const uint32_t hi = __builtin_amdgcn_perm(a47, a03, tb.x);
 							const uint32_t x3 = (hi & tb.y) | (lo & ~tb.y);  // bytes 0..2 = x, y, z
-							const int vt = (int)(__builtin_amdgcn_udot4(x3, 0x00010201u, 2u, false) >> 2);
-							const int vtm = sat8((int)__builtin_amdgcn_udot4(x3, 0x00010001u, 0u, false) - (int)((x3 >> 8) & 0xFFu));
+							// directional modes and TM in one signed dot product over the byte-biased edge
+							const int vdir = sat8(__builtin_amdgcn_sdot4((int)(x3 ^ 0x00808080u), (int)tb.z,
+							                                             (int)(tb.w & 0xFFFFu), false) >> (tb.w >> 16));
 							const int vdc = (int)((__builtin_amdgcn_sad_u8(a03, 0u, __builtin_amdgcn_sad_u8(lw, 0u, 4u))) >> 3);
-							const int pred = mode == 0 ? vdc : (mode == 1 ? vtm : vt);
+							const int pred = mode == 0 ? vdc : vdir;
 							const int px = sat8(pred + rv);
 							tpix[kBS * i0 + 4 * s] = (uint8_t)px;
 							// right pixel column of a sub-block: left column of the next sub-block column (in
