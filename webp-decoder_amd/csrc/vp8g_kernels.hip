@@ -33,6 +33,17 @@
 // Diagnostic builds only (never in the shipped library): VP8G_STAMPS accumulates per-phase
 // shader-clock cycles (s_memtime) into g_vp8g_stamps; VP8G_ABLATE skips phases (timing only,
 // output wrong): 1 = loop filter, 2 = B_PRED steps, 4 = pixel stores, 8 = dependency wait.
+// Wave issue priority per phase (s_setprio 0..3): residual, wait, borders, whole-block
+// prediction, B_PRED, loop filter, flush, publish.  Four waves share a SIMD, each in some phase
+// of its step: the latency-bound phases (chains of dependent LDS round trips, above all the
+// 10-step B_PRED wavefront) issue ahead of the throughput-bound ones (the residual transform
+// and the loop filter, long runs of independent VALU), which then fill the gaps.  Measured on
+// 512 x 4K (tools/abn.sh, one box): all 0 -> 17.7 ms; B_PRED 2 -> 17.2; this table -> 15.6.
+#ifndef VP8G_PRIO_TABLE
+#define VP8G_PRIO_TABLE 0, 2, 2, 3, 3, 1, 2, 2
+#endif
+constexpr int kPrioTab[8] = {VP8G_PRIO_TABLE};
+#define PRIO(ph) __builtin_amdgcn_s_setprio(kPrioTab[ph])
 #ifndef VP8G_ABLATE
 #define VP8G_ABLATE 0
 #endif
@@ -462,7 +473,6 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 	const uint64_t mb0 = D.mb_offset;
 	uint8_t* const outY = out + D.out_y;
 	uint8_t* const outU = out + D.out_u;
-	uint8_t* const outV = out + D.out_v;
 	const uint32_t W = D.width, H = D.height, CW = (D.width + 1) >> 1, CH = (D.height + 1) >> 1;
 	const uint32_t sy = D.stride_y, suv = D.stride_uv;
 	const uint32_t vofs = (uint32_t)(D.out_v - D.out_u);  // V plane relative to U (< 2^32 by construction)
@@ -578,6 +588,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			const uint32_t y0 = r * 16, cy0 = r * 8, x0 = cu * 16, cx0 = cu * 8;
 
 			// ---------------------------------------------- residual (no spatial dependency)
+			PRIO(0);
 			// Computed before the dependency wait.  Each block stays in its lane's registers (rs[],
 			// packed int16 pairs) for the whole-block predictors of the same lane; the luma blocks
 			// are also parked in LDS (kResid) for the B_PRED pixel lanes.
@@ -661,6 +672,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			STAMP(0);
 
 			// ---------------------------------------------- wait: pair k-1's lower row 2 cols ahead
+			PRIO(1);
 			if (k > 0 && !(VP8G_ABLATE & 8)) {
 				const uint32_t need = (k - 1) * CP2 + ((t + 4 < CP2) ? t + 4 : CP2);
 				const uint32_t pw = (uint32_t)((wave + NW - 1) % NW);
@@ -682,6 +694,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			STAMP(1);
 
 			// ---------------------------------------------- borders + loop-filter top strip
+			PRIO(2);
 			if (act) {
 				const bool top = r == 0;
 				if (lf_only) {
@@ -729,6 +742,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			STAMP(2);
 
 			// ---------------------------------------------- prediction + reconstruction
+			PRIO(3);
 			if (!lf_only) {
 				if (act && ln < 24 && (ln >= 16 || !bpred)) {
 					// whole-block predictors (RFC 12.2; reference vp8_recon.c:152-212, 533-560, 605-651),
@@ -786,6 +800,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 				SUBMARK(20);
 				const bool bp_lane = act && bpred;
 				if (__ballot(bp_lane) != 0ull && !(VP8G_ABLATE & 2)) {
+					PRIO(4);
 					// B_PRED: 16 sub-blocks along the 2i+j wavefront (10 steps, <= 2 sub-blocks each;
 					// lanes 0..15 / 16..31 of a half = group g take sub-block (i0 + g, s - 2 i0 - 2 g)),
 					// one pixel per lane, from already reconstructed pixels (reference
@@ -858,6 +873,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			STAMP(4);
 
 			// ---------------------------------------------- loop filter MB(r, c)
+			PRIO(5);
 			if (lf_on && !(VP8G_ABLATE & 1)) {
 				const uint8_t* lp = smem + kLfTable + seg * 8 + (bpred ? 4 : 0);
 				const int E = lp[0], I = lp[1], Tt = lp[2];
@@ -871,6 +887,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			STAMP(5);
 
 			// ---------------------------------------------- store final pixels
+			PRIO(6);
 			// One row piece per lane (luma 16 B, chroma 8 B) from LDS to the output plane or, for the
 			// bottom rows the next MB row still filters, to ctx_lf.  Straight-line: the crop / odd
 			// alignment case (a partial row piece at the right edge) is a rare wave-uniform branch.
@@ -983,6 +1000,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			STAMP(6);
 
 			// ---------------------------------------------- publish progress
+			PRIO(7);
 			ctx.publish_fence();
 			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 			if (lane == 0) __hip_atomic_store(prog + wave, k * CP2 + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
