@@ -42,7 +42,13 @@
 #ifndef VP8G_PRIO_TABLE
 #define VP8G_PRIO_TABLE 0, 2, 2, 3, 3, 1, 2, 2
 #endif
-constexpr int kPrioTab[8] = {VP8G_PRIO_TABLE};
+#ifndef VP8G_PRIO_LF  // loop filter: gather (LDS round trip), edge arithmetic
+#define VP8G_PRIO_LF 1, 1
+#endif
+#ifndef VP8G_PRIO_WHT  // the iWHT's two LDS round trips inside the residual phase
+#define VP8G_PRIO_WHT 2
+#endif
+constexpr int kPrioTab[11] = {VP8G_PRIO_TABLE, VP8G_PRIO_LF, VP8G_PRIO_WHT};
 #define PRIO(ph) __builtin_amdgcn_s_setprio(kPrioTab[ph])
 #ifndef VP8G_ABLATE
 #define VP8G_ABLATE 0
@@ -404,7 +410,9 @@ DEV void lf_mb(uint8_t* tY, uint8_t* tC, int ln, int slot, bool en, bool mb_v, b
 		const int off = isy ? slot * 16 : slot * 8, ring = isy ? 31 : 15;
 		uint8_t* const Lp = rowp + ((off - 4) & ring);
 		uint8_t* const Mp = rowp + off;
+		PRIO(8);
 		gather20<1, 1>(Lp, Mp, px);
+		PRIO(9);
 		lf_line<kSimple>(px, en && mb_v, en && inner, isy, E, I, T);
 		if (wr) {
 #pragma unroll
@@ -421,7 +429,9 @@ DEV void lf_mb(uint8_t* tY, uint8_t* tC, int ln, int slot, bool en, bool mb_v, b
 	// horizontal edges: one line per lane down a pixel column (tile rows 0..19, pitch kTP)
 	{
 		uint8_t* const colp = isy ? tY + slot * 16 + ln : tC + cp * 16 + slot * 8 + (ln & 7);
+		PRIO(8);
 		gather20<kTP, kTP>(colp, colp + 4 * kTP, px);
+		PRIO(9);
 		lf_line<kSimple>(px, en && mb_h, en && inner, isy, E, I, T);
 		if (wr) {
 #pragma unroll
@@ -612,6 +622,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 				// packed in lanes 26 / 27 (column pairs 0-1 / 2-3), the horizontal pass one row per
 				// lane in 26..29, through kWht.
 				if (__ballot(act && !bpred) != 0ull) {
+					PRIO(10);
 					const bool wl = ln >= 26 && ln < 30;
 					{
 						const int h = ln & 1;
@@ -635,6 +646,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					}
 					wave_lds_sync();
 					if (ln < 16 && !bpred) w[0] = (w[0] & 0xFFFF0000u) | *(const uint16_t*)(hv + kWht + 2 * ln);
+					PRIO(0);
 				}
 				// inverse DCT (RFC 14.4), whole 4x4 block per lane; DC-only shortcut when no lane
 				// of the wave has an AC coefficient ((dc+4)>>3 everywhere, exact)
