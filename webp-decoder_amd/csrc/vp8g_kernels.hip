@@ -790,14 +790,26 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					const uint32_t A01 = pk_add(__builtin_amdgcn_perm(aw, aw, 0x0C010C00u) & mA, K2);
 					const uint32_t A23 = pk_add(__builtin_amdgcn_perm(aw, aw, 0x0C030C02u) & mA, K2);
 					uint32_t wv[4];
+					// only TM_PRED's predictor can leave [0, 255]: its clamp runs when some lane uses it
+					if (__ballot(mode == 3) != 0ull) {
 #pragma unroll
-					for (int rr = 0; rr < 4; rr++) {
-						const uint32_t L2 = __builtin_amdgcn_perm(lw, lw, 0x0C000C00u + 0x00010001u * rr) & mL;
-						const uint32_t p01 = pk_clamp255(pk_add(pk_clamp255(pk_add(L2, A01)), rw[2 * rr]));
-						const uint32_t p23 = pk_clamp255(pk_add(pk_clamp255(pk_add(L2, A23)), rw[2 * rr + 1]));
-						wv[rr] = __builtin_amdgcn_perm(p23, p01, 0x06040200u);
-						st32(dst + rr * kTP, wv[rr]);
+						for (int rr = 0; rr < 4; rr++) {
+							const uint32_t L2 = __builtin_amdgcn_perm(lw, lw, 0x0C000C00u + 0x00010001u * rr) & mL;
+							const uint32_t p01 = pk_clamp255(pk_add(pk_clamp255(pk_add(L2, A01)), rw[2 * rr]));
+							const uint32_t p23 = pk_clamp255(pk_add(pk_clamp255(pk_add(L2, A23)), rw[2 * rr + 1]));
+							wv[rr] = __builtin_amdgcn_perm(p23, p01, 0x06040200u);
+						}
+					} else {
+#pragma unroll
+						for (int rr = 0; rr < 4; rr++) {
+							const uint32_t L2 = __builtin_amdgcn_perm(lw, lw, 0x0C000C00u + 0x00010001u * rr) & mL;
+							const uint32_t p01 = pk_clamp255(pk_add(pk_add(L2, A01), rw[2 * rr]));
+							const uint32_t p23 = pk_clamp255(pk_add(pk_add(L2, A23), rw[2 * rr + 1]));
+							wv[rr] = __builtin_amdgcn_perm(p23, p01, 0x06040200u);
+						}
 					}
+#pragma unroll
+					for (int rr = 0; rr < 4; rr++) st32(dst + rr * kTP, wv[rr]);
 					// the MB's unfiltered bottom row -> ctx_rec[c] (the next MB row's above row) and its
 					// right column -> the left column of the next MB (reference vp8_recon.c:395-421)
 					const int last = yl ? 3 : 1;
