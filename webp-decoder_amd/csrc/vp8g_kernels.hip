@@ -288,13 +288,15 @@ DEV uint32_t lf_off(uint32_t c) { return __umul24(c, (uint32_t)kCtxBytesPerCol) 
 // ---------------------------------------------------------------------------------------------
 // normal-filter edge mask (RFC 15.3 filter_yes + interior limits) and high-edge-variance
 DEV void edge_mask(const int* x, bool en, int lim, int I, int T, bool& m, bool& hev) {
-	const int d10 = ad(x[2], x[3]), e10 = ad(x[5], x[4]);
-	const int interior = max(max3i(ad(x[0], x[1]), ad(x[1], x[2]), d10), max3i(ad(x[7], x[6]), ad(x[6], x[5]), e10));
+	const int hm = max(ad(x[2], x[3]), ad(x[5], x[4]));  // max(|p1-p0|, |q1-q0|), shared with hev
+	const int interior = max3i(max3i(ad(x[0], x[1]), ad(x[1], x[2]), ad(x[7], x[6])), ad(x[6], x[5]), hm);
 	const bool fy = ad(x[3], x[4]) * 2 + (ad(x[2], x[5]) >> 1) <= lim;
 	m = en & fy & (interior <= I);
-	hev = max(d10, e10) > T;
+	hev = hm > T;
 }
 
+// Pixel updates are written as sat8(pixel +- masked delta): a masked-off delta is 0 and leaves
+// the pixel unchanged, so one select per delta (shared by the p and q side) replaces one per pixel.
 DEV void lf_mb_edge(int* x, bool en, int lim, int I, int T) {  // normal, MB edge
 	bool m, hev;
 	edge_mask(x, en, lim, I, T, m, hev);
@@ -302,14 +304,15 @@ DEV void lf_mb_edge(int* x, bool en, int lim, int I, int T) {  // normal, MB edg
 	const int w = sclamp(sclamp(p1 - q1) + __mul24(q0 - p0, 3));
 	const int f1 = sclamp(w + 4) >> 3, f2 = sclamp(w + 3) >> 3;
 	const int a27 = (27 * w + 63) >> 7, a18 = (18 * w + 63) >> 7, a9 = (9 * w + 63) >> 7;
-	const bool mh = m & hev, mn = m & !hev;
-	const int d0p = mh ? f2 : a27, d0q = mh ? f1 : a27;
-	x[3] = m ? sat8(p0 + d0p) : p0;
-	x[4] = m ? sat8(q0 - d0q) : q0;
-	x[2] = mn ? sat8(p1 + a18) : p1;
-	x[5] = mn ? sat8(q1 - a18) : q1;
-	x[1] = mn ? sat8(p2 + a9) : p2;
-	x[6] = mn ? sat8(q2 - a9) : q2;
+	const bool mn = m & !hev;
+	const int d0p = m ? (hev ? f2 : a27) : 0, d0q = m ? (hev ? f1 : a27) : 0;
+	const int d1 = mn ? a18 : 0, d2 = mn ? a9 : 0;
+	x[3] = sat8(p0 + d0p);
+	x[4] = sat8(q0 - d0q);
+	x[2] = sat8(p1 + d1);
+	x[5] = sat8(q1 - d1);
+	x[1] = sat8(p2 + d2);
+	x[6] = sat8(q2 - d2);
 }
 
 DEV void lf_sub_edge(int* x, bool en, int lim, int I, int T) {  // normal, sub-block edge
@@ -318,12 +321,12 @@ DEV void lf_sub_edge(int* x, bool en, int lim, int I, int T) {  // normal, sub-b
 	const int p1 = x[2], p0 = x[3], q0 = x[4], q1 = x[5];
 	const int a = sclamp(__mul24(q0 - p0, 3) + (hev ? sclamp(p1 - q1) : 0));
 	const int f1 = sclamp(a + 4) >> 3, f2 = sclamp(a + 3) >> 3;
-	const int a2 = (f1 + 1) >> 1;
 	const bool mn = m & !hev;
-	x[4] = m ? sat8(q0 - f1) : q0;
-	x[3] = m ? sat8(p0 + f2) : p0;
-	x[5] = mn ? sat8(q1 - a2) : q1;
-	x[2] = mn ? sat8(p1 + a2) : p1;
+	const int f1m = m ? f1 : 0, f2m = m ? f2 : 0, a2m = mn ? (f1 + 1) >> 1 : 0;
+	x[4] = sat8(q0 - f1m);
+	x[3] = sat8(p0 + f2m);
+	x[5] = sat8(q1 - a2m);
+	x[2] = sat8(p1 + a2m);
 }
 
 DEV void lf_simple_edge(int* x, bool en, int lim) {  // simple filter (luma only)
