@@ -144,9 +144,9 @@ constexpr BpTab make_bptab() {
 			// value = (sdot4(E_xyz - 128, w) + bias) >> sh  (avg3: (1, 2, 1), 514, 2; TM: (1, -1, 1), 128, 0)
 			const bool tm = m == 1;
 			t.v[(m * 16 + p) * 4] = sel;
-			t.v[(m * 16 + p) * 4 + 1] = mask;
+			t.v[(m * 16 + p) * 4 + 1] = mask | ((tm ? 0u : 2u) << 24);  // byte 3: the shift (x3's byte 3 is unused)
 			t.v[(m * 16 + p) * 4 + 2] = tm ? 0x0001FF01u : 0x00010201u;
-			t.v[(m * 16 + p) * 4 + 3] = tm ? 128u : (514u | (2u << 16));
+			t.v[(m * 16 + p) * 4 + 3] = tm ? 128u : 514u;
 		}
 	return t;
 }
@@ -876,8 +876,8 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 							const uint32_t hi = __builtin_amdgcn_perm(a47, a03, tb.x);
 							const uint32_t x3 = (hi & tb.y) | (lo & ~tb.y);  // bytes 0..2 = x, y, z
 							// directional modes and TM in one signed dot product over the byte-biased edge
-							const int vdir = sat8(__builtin_amdgcn_sdot4((int)(x3 ^ 0x00808080u), (int)tb.z,
-							                                             (int)(tb.w & 0xFFFFu), false) >> (tb.w >> 16));
+							const int vdir = sat8(__builtin_amdgcn_sdot4((int)(x3 ^ 0x00808080u), (int)tb.z, (int)tb.w, false) >>
+							                      (tb.y >> 24));
 							const int vdc = (int)((__builtin_amdgcn_sad_u8(a03, 0u, __builtin_amdgcn_sad_u8(lw, 0u, 4u))) >> 3);
 							const int pred = mode == 0 ? vdc : vdir;
 							const int px = sat8(pred + rv);
