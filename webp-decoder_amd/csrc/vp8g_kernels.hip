@@ -186,8 +186,17 @@ DEV void wave_lds_sync() { asm volatile("" ::: "memory"); }
 DEV int sx16(int x) { return (int)(int16_t)x; }
 DEV int sat8(int v) { return min(max(v, 0), 255); }  // v_med3_i32
 DEV int sclamp(int v) { return min(max(v, -128), 127); }
+// sclamp(sclamp(x) + k) >> 3 for k = 3, 4 (RFC 15.2 common_adjust), as one v_med3 with inline
+// bounds after the shift: both forms give (x + k) >> 3 clamped to [-16, 15]
+DEV int fshift(int x, int k) { return min(max((x + k) >> 3, -16), 15); }
 DEV int ad(int a, int b) { return (int)__builtin_amdgcn_sad_u16((uint32_t)a, (uint32_t)b, 0u); }  // |a-b| for 0 <= a,b < 65536
 DEV int max3i(int a, int b, int c) { return max(a, max(b, c)); }
+// v_max3_u32 pinned (the compiler re-associates max chains into more two-input maxes)
+DEV int max3u(int a, int b, int c) {
+	int r;
+	asm("v_max3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+	return r;
+}
 DEV int mul_s(int x) { return (x * 35468) >> 16; }        // x*sqrt(2)*sin(pi/8), RFC 14.4
 DEV int mul_c(int x) { return x + ((x * 20091) >> 16); }  // x*sqrt(2)*cos(pi/8)
 DEV uint32_t bsum4(uint32_t w) { return __builtin_amdgcn_sad_u8(w, 0u, 0u); }
@@ -289,7 +298,7 @@ DEV uint32_t lf_off(uint32_t c) { return __umul24(c, (uint32_t)kCtxBytesPerCol) 
 // normal-filter edge mask (RFC 15.3 filter_yes + interior limits) and high-edge-variance
 DEV void edge_mask(const int* x, bool en, int lim, int I, int T, bool& m, bool& hev) {
 	const int hm = max(ad(x[2], x[3]), ad(x[5], x[4]));  // max(|p1-p0|, |q1-q0|), shared with hev
-	const int interior = max3i(max3i(ad(x[0], x[1]), ad(x[1], x[2]), ad(x[7], x[6])), ad(x[6], x[5]), hm);
+	const int interior = max3u(max3u(ad(x[0], x[1]), ad(x[1], x[2]), ad(x[7], x[6])), ad(x[6], x[5]), hm);
 	const bool fy = ad(x[3], x[4]) * 2 + (ad(x[2], x[5]) >> 1) <= lim;
 	m = en & fy & (interior <= I);
 	hev = hm > T;
@@ -319,8 +328,8 @@ DEV void lf_sub_edge(int* x, bool en, int lim, int I, int T) {  // normal, sub-b
 	bool m, hev;
 	edge_mask(x, en, lim, I, T, m, hev);
 	const int p1 = x[2], p0 = x[3], q0 = x[4], q1 = x[5];
-	const int a = sclamp(__mul24(q0 - p0, 3) + (hev ? sclamp(p1 - q1) : 0));
-	const int f1 = sclamp(a + 4) >> 3, f2 = sclamp(a + 3) >> 3;
+	const int a = __mul24(q0 - p0, 3) + (hev ? sclamp(p1 - q1) : 0);
+	const int f1 = fshift(a, 4), f2 = fshift(a, 3);
 	const bool mn = m & !hev;
 	const int f1m = m ? f1 : 0, f2m = m ? f2 : 0, a2m = mn ? (f1 + 1) >> 1 : 0;
 	x[4] = sat8(q0 - f1m);
@@ -332,9 +341,9 @@ DEV void lf_sub_edge(int* x, bool en, int lim, int I, int T) {  // normal, sub-b
 DEV void lf_simple_edge(int* x, bool en, int lim) {  // simple filter (luma only)
 	const int p1 = x[2], p0 = x[3], q0 = x[4], q1 = x[5];
 	const bool m = en & (ad(p0, q0) * 2 + (ad(p1, q1) >> 1) <= lim);
-	const int a = sclamp(sclamp(p1 - q1) + __mul24(q0 - p0, 3));
-	x[4] = m ? sat8(q0 - (sclamp(a + 4) >> 3)) : q0;
-	x[3] = m ? sat8(p0 + (sclamp(a + 3) >> 3)) : p0;
+	const int a = sclamp(p1 - q1) + __mul24(q0 - p0, 3);
+	x[4] = m ? sat8(q0 - fshift(a, 4)) : q0;
+	x[3] = m ? sat8(p0 + fshift(a, 3)) : p0;
 }
 
 // All edges of one line, in the reference order (MB edge, then sub-block edges).  `is_y`
