@@ -304,18 +304,18 @@ DEV void edge_mask(const int* x, bool en, int lim, int I, int T, bool& m, bool& 
 	hev = hm > T;
 }
 
-// Pixel updates are written as sat8(pixel +- masked delta): a masked-off delta is 0 and leaves
-// the pixel unchanged, so one select per delta (shared by the p and q side) replaces one per pixel.
+// Masking: the filter input (the common-adjust value) is zeroed where the edge mask is off, which
+// makes every tap 0 ((0 + 4) >> 3 = (0 + 3) >> 3 = (0 + 63) >> 7 = 0), so one select per edge
+// replaces one per delta and the pixel updates sat8(pixel +- delta) run unconditionally.
 DEV void lf_mb_edge(int* x, bool en, int lim, int I, int T) {  // normal, MB edge
 	bool m, hev;
 	edge_mask(x, en, lim, I, T, m, hev);
 	const int p2 = x[1], p1 = x[2], p0 = x[3], q0 = x[4], q1 = x[5], q2 = x[6];
-	const int w = sclamp(sclamp(p1 - q1) + __mul24(q0 - p0, 3));
+	const int w = sclamp(m ? sclamp(p1 - q1) + __mul24(q0 - p0, 3) : 0);
 	const int f1 = sclamp(w + 4) >> 3, f2 = sclamp(w + 3) >> 3;
 	const int a27 = (27 * w + 63) >> 7, a18 = (18 * w + 63) >> 7, a9 = (9 * w + 63) >> 7;
-	const bool mn = m & !hev;
-	const int d0p = m ? (hev ? f2 : a27) : 0, d0q = m ? (hev ? f1 : a27) : 0;
-	const int d1 = mn ? a18 : 0, d2 = mn ? a9 : 0;
+	const int d0p = hev ? f2 : a27, d0q = hev ? f1 : a27;
+	const int d1 = hev ? 0 : a18, d2 = hev ? 0 : a9;
 	x[3] = sat8(p0 + d0p);
 	x[4] = sat8(q0 - d0q);
 	x[2] = sat8(p1 + d1);
@@ -328,20 +328,19 @@ DEV void lf_sub_edge(int* x, bool en, int lim, int I, int T) {  // normal, sub-b
 	bool m, hev;
 	edge_mask(x, en, lim, I, T, m, hev);
 	const int p1 = x[2], p0 = x[3], q0 = x[4], q1 = x[5];
-	const int a = __mul24(q0 - p0, 3) + (hev ? sclamp(p1 - q1) : 0);
+	const int a = m ? __mul24(q0 - p0, 3) + (hev ? sclamp(p1 - q1) : 0) : 0;
 	const int f1 = fshift(a, 4), f2 = fshift(a, 3);
-	const bool mn = m & !hev;
-	const int f1m = m ? f1 : 0, f2m = m ? f2 : 0, a2m = mn ? (f1 + 1) >> 1 : 0;
-	x[4] = sat8(q0 - f1m);
-	x[3] = sat8(p0 + f2m);
-	x[5] = sat8(q1 - a2m);
-	x[2] = sat8(p1 + a2m);
+	const int a2 = hev ? 0 : (f1 + 1) >> 1;
+	x[4] = sat8(q0 - f1);
+	x[3] = sat8(p0 + f2);
+	x[5] = sat8(q1 - a2);
+	x[2] = sat8(p1 + a2);
 }
 
 DEV void lf_simple_edge(int* x, bool en, int lim) {  // simple filter (luma only)
 	const int p1 = x[2], p0 = x[3], q0 = x[4], q1 = x[5];
 	const bool m = en & (ad(p0, q0) * 2 + (ad(p1, q1) >> 1) <= lim);
-	const int a = sclamp(p1 - q1) + __mul24(q0 - p0, 3);
+	const int a = sclamp(p1 - q1) + __mul24(q0 - p0, 3);  // (branched over where no lane filters)
 	x[4] = m ? sat8(q0 - fshift(a, 4)) : q0;
 	x[3] = m ? sat8(p0 + fshift(a, 3)) : p0;
 }
