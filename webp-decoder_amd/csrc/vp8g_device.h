@@ -52,7 +52,8 @@ hipError_t launch_frames(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const 
                          uint8_t* d_out, uint32_t ctx_cols, uint32_t max_mb_rows, uint8_t* global_ctx,
                          hipStream_t stream, uint32_t waves_hint);
 
-// Waves per workgroup the launcher would use for this batch (for LDS sizing decisions).
-uint32_t pick_waves(uint32_t waves_hint, uint32_t max_mb_rows);
+// Waves per workgroup the launcher would use for this batch (for LDS sizing decisions):
+// waves_hint if non-zero, else 8, or 16 when n_frames <= the device's CU count.
+uint32_t pick_waves(uint32_t waves_hint, uint32_t max_mb_rows, uint32_t n_frames);
 
 }  // namespace vp8g

@@ -465,9 +465,11 @@ struct Pref {
 // ---------------------------------------------------------------------------------------------
 // The fused kernel.
 // ---------------------------------------------------------------------------------------------
-// Occupancy target: two workgroups (frames) per CU -> 2*NW waves per CU.
+// Occupancy target: two workgroups (frames) per CU at NW <= 8 (2*NW waves per CU); one
+// workgroup of 12 or 16 waves per CU for batches smaller than the CU count (pick_waves).  Either
+// way at most 4 waves per SIMD, i.e. the full 128-VGPR budget.
 template <int NW>
-constexpr int min_waves_per_simd() { return NW >= 2 ? (2 * NW) / 4 : 1; }
+constexpr int min_waves_per_simd() { return NW >= 8 ? 4 : (NW >= 2 ? (2 * NW) / 4 : 1); }
 
 template <int NW, bool kG>
 __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kernel(const Vp8gFrameDesc* __restrict__ descs, Vp8gBatchArrays A,
@@ -1082,9 +1084,17 @@ extern "C" __attribute__((visibility("default"))) int vp8g_debug_stamps(unsigned
 }
 #endif
 
-uint32_t pick_waves(uint32_t waves_hint, uint32_t max_mb_rows) {
+uint32_t pick_waves(uint32_t waves_hint, uint32_t max_mb_rows, uint32_t n_frames) {
 	static const uint32_t kSupported[] = {1, 2, 4, 8, 12, 16};
-	uint32_t want = waves_hint ? waves_hint : 8;
+	// default: 8 waves (two frames per CU) when the batch fills the chip; a batch with at most
+	// one frame per CU gets 16 waves per frame instead (twice the MB row pairs in flight)
+	static const int n_cus = [] {
+		int dev = 0, n = 0;
+		if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+			n = 0;
+		return n;
+	}();
+	uint32_t want = waves_hint ? waves_hint : (n_cus > 0 && n_frames <= (uint32_t)n_cus ? 16u : 8u);
 	const uint32_t pairs = (max_mb_rows + 1) / 2;
 	if (want > pairs) want = pairs;  // no point in more waves than MB row pairs
 	uint32_t nw = 1;
@@ -1097,7 +1107,7 @@ hipError_t launch_frames(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const 
                          uint8_t* d_out, uint32_t ctx_cols, uint32_t max_mb_rows, uint8_t* global_ctx,
                          hipStream_t stream, uint32_t waves_hint) {
 	if (n_frames == 0) return hipSuccess;
-	const uint32_t nw = pick_waves(waves_hint, max_mb_rows);
+	const uint32_t nw = pick_waves(waves_hint, max_mb_rows, n_frames);
 	const bool g = global_ctx != nullptr;
 #define VP8G_CASE(N)                                                                                  \
 	case N:                                                                                           \

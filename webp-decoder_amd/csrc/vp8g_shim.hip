@@ -175,7 +175,7 @@ int run_locked(const std::vector<Vp8gFrameDesc>& descs, const Vp8gBatchArrays& a
 		if (d.mb_cols > max_cols) max_cols = d.mb_cols;
 		if (d.mb_rows > max_rows) max_rows = d.mb_rows;
 	}
-	const uint32_t nw = vp8g::pick_waves(waves_hint, max_rows);
+	const uint32_t nw = vp8g::pick_waves(waves_hint, max_rows, (uint32_t)descs.size());
 	uint8_t* gctx = nullptr;
 	if (vp8g::lds_bytes((int)nw, max_cols, false) > (size_t)vp8g::kMaxLds) {
 		const size_t need = descs.size() * (size_t)max_cols * vp8g::kCtxBytesPerCol;
