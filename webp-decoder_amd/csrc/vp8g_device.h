@@ -48,9 +48,18 @@ inline size_t lds_bytes(int waves, uint32_t ctx_cols, bool global_ctx) {
 // Launch the fused recon(+LF) kernel.  `global_ctx` != nullptr selects the variant whose
 // per-column context lives in device memory (frames too wide for LDS); it must hold
 // n_frames * ctx_cols * kCtxBytesPerCol bytes.
+// nsplit > 1 (LDS context, 8 or 16 waves only): each frame is worked on by nsplit workgroups
+// that hand off through `mbox` (n_frames * nsplit * ctx_cols * kCtxBytesPerCol bytes) and
+// `gprog` (n_frames * nsplit words, zeroed before the launch).
 hipError_t launch_frames(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const Vp8gBatchArrays& arrays,
                          uint8_t* d_out, uint32_t ctx_cols, uint32_t max_mb_rows, uint8_t* global_ctx,
-                         hipStream_t stream, uint32_t waves_hint);
+                         hipStream_t stream, uint32_t waves_hint, uint32_t nsplit, uint8_t* mbox, uint32_t* gprog);
+
+constexpr uint32_t kMaxSplit = 8;
+int device_cus();
+// Workgroups per frame for this batch: split_hint if non-zero, else CUs / frames, capped at
+// kMaxSplit and at one part per CU overall (all parts must be co-resident), 1 if not possible.
+uint32_t pick_split(uint32_t split_hint, uint32_t n_frames, uint32_t nw, uint32_t max_mb_rows);
 
 // Waves per workgroup the launcher would use for this batch (for LDS sizing decisions):
 // waves_hint if non-zero, else 8, or 16 when n_frames <= the device's CU count.

@@ -471,14 +471,28 @@ struct Pref {
 template <int NW>
 constexpr int min_waves_per_simd() { return NW >= 8 ? 4 : (NW >= 2 ? (2 * NW) / 4 : 1); }
 
-template <int NW, bool kG>
+// Split mode (kS, small batches): a frame's MB row pairs are dealt over `nsplit` workgroups
+// ("parts") of NW waves each -- global wave g = part * NW + wave owns pairs g, g + nsplit*NW, ...
+// Inside a part the waves hand off through LDS as above.  Across parts (wave 0 of part j waits on
+// wave NW-1 of part j-1) the hand-off is a mailbox in device memory, one channel per part, laid
+// out like ctx (rec + lf per column): the producer copies each column's finished ctx entry with
+// write-through (sc1) stores, drains them (vmcnt(0)) and then stores its progress word with an
+// agent-scope atomic; the consumer polls that word and reads the mailbox with sc1 loads, one step
+// ahead of use (MI355X_MICROARCH.md, inter-workgroup visibility: sc1 payload + drained flag).
+// Requires every part of a frame to be resident at once: the host splits only batches of at most
+// one part per CU.
+template <int NW, bool kG, bool kS>
 __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kernel(const Vp8gFrameDesc* __restrict__ descs, Vp8gBatchArrays A,
                                                         uint8_t* __restrict__ out, uint32_t ctx_cols,
-                                                        uint8_t* __restrict__ gctx) {
+                                                        uint8_t* __restrict__ gctx, uint32_t nsplit,
+                                                        uint8_t* __restrict__ mbox, uint32_t* __restrict__ gprog) {
 	extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 	const int lane0 = (int)(threadIdx.x & 63);
 	const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-	const uint32_t f = blockIdx.x;
+	const uint32_t K = kS ? nsplit : 1u;
+	const uint32_t nfr = kS ? gridDim.x / K : gridDim.x;
+	const uint32_t f = kS ? blockIdx.x % nfr : blockIdx.x;
+	const uint32_t part = kS ? blockIdx.x / nfr : 0u;
 	const Vp8gFrameDesc& D = descs[f];
 
 	for (int i = (int)threadIdx.x; i < kBpModes * 64; i += NW * 64) ((uint32_t*)(smem + kBpTable))[i] = kBpTab.v[i];
@@ -506,6 +520,13 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 	ctx.g = kG ? gctx + (size_t)f * ctx_cols * kCtxBytesPerCol : nullptr;
 	const uint32_t npairs = (R + 1) >> 1;
 	const uint32_t CP2 = C + 2;
+	const uint32_t GW = K * NW, gw = part * NW + (uint32_t)wave;
+	const size_t chan = (size_t)ctx_cols * kCtxBytesPerCol;
+	const uint32_t pin = (part + K - 1) % K;  // the part holding this part's wave-0 predecessors
+	uint8_t* const mb_in = kS ? mbox + (f * K + pin) * chan : nullptr;
+	uint8_t* const mb_out = kS ? mbox + (f * K + part) * chan : nullptr;
+	uint32_t* const gp_in = kS ? gprog + f * K + pin : nullptr;
+	uint32_t* const gp_out = kS ? gprog + f * K + part : nullptr;
 
 #ifdef VP8G_STAMPS
 	uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -532,7 +553,10 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 		return p;
 	};
 
-	for (uint32_t k = (uint32_t)wave; k < npairs; k += NW) {
+	for (uint32_t k = gw; k < npairs; k += GW) {
+		const bool xin = kS && wave == 0 && k > 0;             // predecessor pair in another part
+		const bool xout = kS && wave == NW - 1 && k + 1 < npairs;  // successor pair in another part
+		u32x4 mbx = u32x4{0u, 0u, 0u, 0u};                     // mailbox prefetch (xin: lanes 0..9)
 		const uint32_t rA = 2 * k;
 		const bool two = rA + 1 < R;
 		const uint32_t T = two ? CP2 : C;
@@ -699,11 +723,14 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			// ---------------------------------------------- wait: pair k-1's lower row 2 cols ahead
 			PRIO(1);
 			if (k > 0 && !(VP8G_ABLATE & 8)) {
-				const uint32_t need = (k - 1) * CP2 + ((t + 4 < CP2) ? t + 4 : CP2);
+				// (one column more lag across parts: the mailbox is read a step ahead of use)
+				const uint32_t lag = xin ? 5u : 4u;
+				const uint32_t need = (k - 1) * CP2 + ((t + lag < CP2) ? t + lag : CP2);
 				const uint32_t pw = (uint32_t)((wave + NW - 1) % NW);
 				uint32_t spins = 0;
 				uint64_t t0 = 0;
-				while (__hip_atomic_load(prog + pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+				while ((xin ? __hip_atomic_load(gp_in, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+				            : __hip_atomic_load(prog + pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < need) {
 					__builtin_amdgcn_s_sleep(1);
 					if ((++spins & 1023u) == 0) {
 						const uint64_t now = __builtin_amdgcn_s_memrealtime();
@@ -715,6 +742,30 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					}
 				}
 				asm volatile("" ::: "memory");
+			}
+			if (kS && xin) {
+				// mailbox -> this part's LDS ctx: rec[t + 1] and lf[t] now (loaded last step; at t = 0
+				// rec[0], rec[1], lf[0] directly), then the loads for the next step (lane roles: ln 0..1
+				// the 32-B rec entry, 2..9 the 128-B lf entry, as 16-B pieces)
+				auto mload = [&](uint32_t col, uint32_t o) -> u32x4 {
+					const uint32_t* q = (const uint32_t*)(mb_in + (size_t)col * kCtxBytesPerCol + o);
+					return u32x4{__hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+					             __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+					             __hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+					             __hip_atomic_load(q + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)};
+				};
+				const uint32_t o = 16u * (uint32_t)(lane0 & 15);  // byte offset in the column entry
+				if (t == 0) {
+					// ln 0..9: column 0 (rec + lf), 10..11: rec of column 1
+					const uint32_t col = lane0 < 10 ? 0u : 1u, oo = lane0 < 10 ? o : o - 160u;
+					if (lane0 < 12 && col < C) st128(ctx.lds + col * kCtxBytesPerCol + oo, mload(col, oo));
+				} else {
+					const uint32_t col = lane0 < 2 ? t + 1 : t;
+					if (lane0 < 10 && col < C) st128(ctx.lds + col * kCtxBytesPerCol + o, mbx);
+				}
+				const uint32_t ncol = lane0 < 2 ? t + 2 : t + 1;
+				if (lane0 < 10 && ncol < C) mbx = mload(ncol, o);
+				wave_lds_sync();
 			}
 			STAMP(1);
 
@@ -1040,6 +1091,22 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			PRIO(7);
 			ctx.publish_fence();
 			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+			if (kS && xout) {
+				// the ctx entries this step finished (rec of column t - 2, lf of column t - 3, and at the
+				// last step lf of column C - 1) -> mailbox, write-through; drained before the flag
+				const int cl = lane0 < 2 ? (int)t - 2 : (lane0 < 10 ? (int)t - 3 : (t + 1 == T ? (int)C - 1 : -1));
+				const uint32_t o = lane0 < 2 ? 16u * (uint32_t)lane0 : 32u + 16u * (uint32_t)((lane0 - 2) & 7);
+				if (lane0 < 18 && cl >= 0 && cl < (int)C) {
+					const u32x4 v = ld128(ctx.lds + (uint32_t)cl * kCtxBytesPerCol + o);
+					uint32_t* q = (uint32_t*)(mb_out + (size_t)cl * kCtxBytesPerCol + o);
+					__hip_atomic_store(q, v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+					__hip_atomic_store(q + 1, v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+					__hip_atomic_store(q + 2, v.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+					__hip_atomic_store(q + 3, v.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+				}
+				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+				if (lane == 0) __hip_atomic_store(gp_out, k * CP2 + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			}
 			if (lane == 0) __hip_atomic_store(prog + wave, k * CP2 + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 			STAMP(7);
 		}
@@ -1055,16 +1122,17 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 #endif
 }
 
-template <int NW, bool kG>
+template <int NW, bool kG, bool kS>
 hipError_t launch_t(const Vp8gFrameDesc* d_descs, uint32_t n, const Vp8gBatchArrays& arrays, uint8_t* d_out,
-                    uint32_t ctx_cols, uint8_t* gctx, hipStream_t stream) {
+                    uint32_t ctx_cols, uint8_t* gctx, uint32_t nsplit, uint8_t* mbox, uint32_t* gprog, hipStream_t stream) {
 	const size_t lds = lds_bytes(NW, ctx_cols, kG);
-	auto fn = frame_kernel<NW, kG>;
+	auto fn = frame_kernel<NW, kG, kS>;
 	if (lds > 65536) {
 		hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
 		if (e != hipSuccess) return e;
 	}
-	hipLaunchKernelGGL(fn, dim3(n), dim3(NW * 64), lds, stream, d_descs, arrays, d_out, ctx_cols, gctx);
+	hipLaunchKernelGGL(fn, dim3(n * (kS ? nsplit : 1u)), dim3(NW * 64), lds, stream, d_descs, arrays, d_out, ctx_cols, gctx,
+	                   nsplit, mbox, gprog);
 	return hipGetLastError();
 }
 
@@ -1084,16 +1152,21 @@ extern "C" __attribute__((visibility("default"))) int vp8g_debug_stamps(unsigned
 }
 #endif
 
-uint32_t pick_waves(uint32_t waves_hint, uint32_t max_mb_rows, uint32_t n_frames) {
-	static const uint32_t kSupported[] = {1, 2, 4, 8, 12, 16};
-	// default: 8 waves (two frames per CU) when the batch fills the chip; a batch with at most
-	// one frame per CU gets 16 waves per frame instead (twice the MB row pairs in flight)
+int device_cus() {
 	static const int n_cus = [] {
 		int dev = 0, n = 0;
 		if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
 			n = 0;
 		return n;
 	}();
+	return n_cus;
+}
+
+uint32_t pick_waves(uint32_t waves_hint, uint32_t max_mb_rows, uint32_t n_frames) {
+	static const uint32_t kSupported[] = {1, 2, 4, 8, 12, 16};
+	// default: 8 waves (two frames per CU) when the batch fills the chip; a batch with at most
+	// one frame per CU gets 16 waves per frame instead (twice the MB row pairs in flight)
+	const int n_cus = device_cus();
 	uint32_t want = waves_hint ? waves_hint : (n_cus > 0 && n_frames <= (uint32_t)n_cus ? 16u : 8u);
 	const uint32_t pairs = (max_mb_rows + 1) / 2;
 	if (want > pairs) want = pairs;  // no point in more waves than MB row pairs
@@ -1103,16 +1176,33 @@ uint32_t pick_waves(uint32_t waves_hint, uint32_t max_mb_rows, uint32_t n_frames
 	return nw;
 }
 
+uint32_t pick_split(uint32_t split_hint, uint32_t n_frames, uint32_t nw, uint32_t max_mb_rows) {
+	if (nw != 8 && nw != 16) return 1;  // split kernels exist for these only
+	const int n_cus = device_cus();
+	const uint32_t pairs = (max_mb_rows + 1) / 2;
+	uint32_t k = split_hint ? split_hint : (n_cus > 0 ? (uint32_t)n_cus / (n_frames ? n_frames : 1u) : 1u);
+	if (k > kMaxSplit) k = kMaxSplit;
+	while (k > 1 && (k - 1) * nw >= pairs) k--;  // every part gets at least one pair
+	// all parts of all frames must be resident together: at most one part per CU
+	if (n_cus <= 0 || (uint64_t)n_frames * k > (uint64_t)n_cus) k = 1;
+	return k ? k : 1;
+}
+
 hipError_t launch_frames(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const Vp8gBatchArrays& arrays,
                          uint8_t* d_out, uint32_t ctx_cols, uint32_t max_mb_rows, uint8_t* global_ctx,
-                         hipStream_t stream, uint32_t waves_hint) {
+                         hipStream_t stream, uint32_t waves_hint, uint32_t nsplit, uint8_t* mbox, uint32_t* gprog) {
 	if (n_frames == 0) return hipSuccess;
 	const uint32_t nw = pick_waves(waves_hint, max_mb_rows, n_frames);
 	const bool g = global_ctx != nullptr;
-#define VP8G_CASE(N)                                                                                  \
-	case N:                                                                                           \
-		return g ? launch_t<N, true>(d_descs, n_frames, arrays, d_out, ctx_cols, global_ctx, stream) \
-		         : launch_t<N, false>(d_descs, n_frames, arrays, d_out, ctx_cols, nullptr, stream);
+	if (nsplit > 1 && !g && (nw == 8 || nw == 16)) {
+		if (!mbox || !gprog) return hipErrorInvalidValue;
+		return nw == 8 ? launch_t<8, false, true>(d_descs, n_frames, arrays, d_out, ctx_cols, nullptr, nsplit, mbox, gprog, stream)
+		               : launch_t<16, false, true>(d_descs, n_frames, arrays, d_out, ctx_cols, nullptr, nsplit, mbox, gprog, stream);
+	}
+#define VP8G_CASE(N)                                                                                                          \
+	case N:                                                                                                                   \
+		return g ? launch_t<N, true, false>(d_descs, n_frames, arrays, d_out, ctx_cols, global_ctx, 1, nullptr, nullptr, stream) \
+		         : launch_t<N, false, false>(d_descs, n_frames, arrays, d_out, ctx_cols, nullptr, 1, nullptr, nullptr, stream);
 	switch (nw) {
 		VP8G_CASE(1)
 		VP8G_CASE(2)

@@ -111,6 +111,8 @@ struct DevState {
 	size_t desc_cap = 0;
 	uint8_t* gctx = nullptr;
 	size_t gctx_cap = 0;
+	uint8_t* mbox = nullptr;  // split-mode hand-off mailboxes + progress words (host APIs only)
+	size_t mbox_cap = 0;
 	uint32_t* status = nullptr;
 };
 DevState g_dev;
@@ -167,23 +169,50 @@ InLayout in_layout(uint64_t mbs, uint64_t src_bytes) {
 		}                             \
 	} while (0)
 
-// Launch over device-resident data with the process stream (caller holds g_dev.mu).
+// VP8G_SPLIT=<k>: workgroups per frame (1 = never split); unset: automatic for the host APIs.
+uint32_t split_env() {
+	const char* e = getenv("VP8G_SPLIT");
+	return e ? (uint32_t)strtoul(e, nullptr, 10) : 0u;
+}
+
+// Launch over device-resident data (caller holds g_dev.mu).  `may_split`: the call completes
+// (stream synchronised) before g_dev.mu is released, so the shared split-mode buffers are safe.
 int run_locked(const std::vector<Vp8gFrameDesc>& descs, const Vp8gBatchArrays& arr, uint8_t* d_out, hipStream_t s,
-               uint32_t waves_hint, uint8_t* d_descs) {
+               uint32_t waves_hint, uint8_t* d_descs, bool may_split) {
 	uint32_t max_cols = 0, max_rows = 0;
 	for (const auto& d : descs) {
 		if (d.mb_cols > max_cols) max_cols = d.mb_cols;
 		if (d.mb_rows > max_rows) max_rows = d.mb_rows;
 	}
-	const uint32_t nw = vp8g::pick_waves(waves_hint, max_rows, (uint32_t)descs.size());
+	const uint32_t n = (uint32_t)descs.size();
+	if (!waves_hint) {
+		const char* e = getenv("VP8G_WAVES");  // override of the default waves per workgroup
+		if (e) waves_hint = (uint32_t)strtoul(e, nullptr, 10);
+	}
+	const uint32_t env = split_env();
+	// small batches on the host APIs: 8-wave parts, up to kMaxSplit per frame (measured on one 4K
+	// frame: 8 waves x 8 parts 3.9 ms per call, 16 waves x 1..8 parts 8.1..4.7 ms)
+	uint32_t nw = vp8g::pick_waves(waves_hint, max_rows, n);
+	if ((may_split || env > 1) && env != 1 && !waves_hint && vp8g::pick_split(env, n, 8, max_rows) > 1) nw = 8;
 	uint8_t* gctx = nullptr;
-	if (vp8g::lds_bytes((int)nw, max_cols, false) > (size_t)vp8g::kMaxLds) {
+	const bool big = vp8g::lds_bytes((int)nw, max_cols, false) > (size_t)vp8g::kMaxLds;
+	if (big) {
 		const size_t need = descs.size() * (size_t)max_cols * vp8g::kCtxBytesPerCol;
 		HIP_TRY(grow(&g_dev.gctx, &g_dev.gctx_cap, need), "hipMalloc(ctx)");
 		gctx = g_dev.gctx;
 	}
-	HIP_TRY(vp8g::launch_frames((const Vp8gFrameDesc*)d_descs, (uint32_t)descs.size(), arr, d_out, max_cols, max_rows, gctx,
-	                            s, nw),
+	uint32_t k = 1;
+	if (!big && (may_split || env > 1) && env != 1) k = vp8g::pick_split(env, n, nw, max_rows);
+	uint8_t* mbox = nullptr;
+	uint32_t* gprog = nullptr;
+	if (k > 1) {
+		const size_t mb = (size_t)n * k * max_cols * vp8g::kCtxBytesPerCol, pb = (size_t)n * k * sizeof(uint32_t);
+		HIP_TRY(grow(&g_dev.mbox, &g_dev.mbox_cap, mb + pb), "hipMalloc(mailbox)");
+		mbox = g_dev.mbox;
+		gprog = (uint32_t*)(g_dev.mbox + mb);
+		HIP_TRY(hipMemsetAsync(gprog, 0, pb, s), "memset(progress)");
+	}
+	HIP_TRY(vp8g::launch_frames((const Vp8gFrameDesc*)d_descs, n, arr, d_out, max_cols, max_rows, gctx, s, nw, k, mbox, gprog),
 	        "launch");
 	return 0;
 }
@@ -270,7 +299,7 @@ VP8G_API int vp8g_decode_batch_device(const Vp8gFrameDesc* h_descs, const Vp8gFr
 	}
 	std::vector<Vp8gFrameDesc> v(h_descs, h_descs + n);
 	std::lock_guard<std::mutex> lk(g_dev.mu);
-	return run_locked(v, *arrays, d_out, (hipStream_t)stream, waves, (uint8_t*)d_descs);
+	return run_locked(v, *arrays, d_out, (hipStream_t)stream, waves, (uint8_t*)d_descs, false);
 }
 
 VP8G_API int vp8g_reconstruct_batch(const Vp8KeyFrameHeader* const* kfs, const Vp8DecodedFrame* const* frames, uint32_t n,
@@ -344,7 +373,7 @@ VP8G_API int vp8g_reconstruct_batch(const Vp8KeyFrameHeader* const* kfs, const V
 	arr.bmode = in + L.bm;
 	arr.src = nullptr;
 	arr.status = g_dev.status;
-	if (run_locked(descs, arr, g_dev.out, s, 0, g_dev.desc) != 0) return fail();
+	if (run_locked(descs, arr, g_dev.out, s, 0, g_dev.desc, true) != 0) return fail();
 	for (uint32_t i = 0; i < n; i++) {
 		const Vp8gFrameDesc& d = descs[i];
 		const size_t ysz = (size_t)d.stride_y * d.height, uvsz = (size_t)d.stride_uv * ((d.height + 1) / 2);
@@ -440,7 +469,7 @@ VP8G_API int vp8_loopfilter_apply_keyframe(Yuv420Image* img, const Vp8DecodedFra
 	arr.bmode = nullptr;
 	arr.src = src;
 	arr.status = g_dev.status;
-	if (run_locked(descs, arr, g_dev.out, s, 0, g_dev.desc) != 0) return -1;
+	if (run_locked(descs, arr, g_dev.out, s, 0, g_dev.desc, true) != 0) return -1;
 	HIP_TRY(hipMemcpy2DAsync(img->y, img->stride_y, g_dev.out, img->width, img->width, img->height, hipMemcpyDeviceToHost, s),
 	        "D2H");
 	HIP_TRY(hipMemcpy2DAsync(img->u, img->stride_uv, g_dev.out + desc.out_u, cw, cw, ch, hipMemcpyDeviceToHost, s), "D2H");
