@@ -223,7 +223,13 @@ int run_locked(const std::vector<Vp8gFrameDesc>& descs, const Vp8gBatchArrays& a
 // Reference entry points
 // ---------------------------------------------------------------------------------------------
 
-VP8G_API int yuv420_alloc(Yuv420Image* img, uint32_t width, uint32_t height) {
+// Planes as yuv420_alloc lays them out, left uninitialised: for outputs the D2H overwrites
+// completely (the fill of yuv420_alloc would be a second full pass over fresh pages).
+int alloc_planes(Yuv420Image* img, uint32_t width, uint32_t height, bool init);
+
+VP8G_API int yuv420_alloc(Yuv420Image* img, uint32_t width, uint32_t height) { return alloc_planes(img, width, height, true); }
+
+int alloc_planes(Yuv420Image* img, uint32_t width, uint32_t height, bool init) {
 	if (!img || width == 0 || height == 0) {
 		errno = EINVAL;
 		return -1;
@@ -245,9 +251,11 @@ VP8G_API int yuv420_alloc(Yuv420Image* img, uint32_t width, uint32_t height) {
 		errno = ENOMEM;
 		return -1;
 	}
-	memset(img->y, 0, ysz);
-	memset(img->u, 128, uvsz);
-	memset(img->v, 128, uvsz);
+	if (init) {
+		memset(img->y, 0, ysz);
+		memset(img->u, 128, uvsz);
+		memset(img->v, 128, uvsz);
+	}
 	return 0;
 }
 
@@ -319,7 +327,7 @@ VP8G_API int vp8g_reconstruct_batch(const Vp8KeyFrameHeader* const* kfs, const V
 		outb = align256(outb + vp8g_i420_size(kfs[i]->width, kfs[i]->height));
 	}
 	for (uint32_t i = 0; i < n; i++) {
-		if (yuv420_alloc(&outs[i], kfs[i]->width, kfs[i]->height) != 0) {
+		if (alloc_planes(&outs[i], kfs[i]->width, kfs[i]->height, false) != 0) {
 			for (uint32_t k = 0; k < i; k++) yuv420_free(&outs[k]);
 			return -1;
 		}
