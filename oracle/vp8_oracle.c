@@ -8,6 +8,7 @@
 #include "vp8_oracle.h"
 
 #include <errno.h>
+#include <stdio.h>
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
@@ -540,4 +541,136 @@ double oracle_time_batch(const Vp8KeyFrameHeader* const* kfs, const Vp8DecodedFr
 	free(th);
 	if (j.err || started == 0) return -1.0;
 	return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+
+/* ==== m08 / m09: I420 -> RGB24 ("fancy" 4:2:0 upsampling) and the PPM / PNG writers ========
+ * Restated per output pixel (the reference walks row pairs and pixel pairs; the values are the
+ * same): reference src/m08_yuv2rgb_ppm/yuv2rgb_ppm.c:13-121 (conversion + upsampler),
+ * :123-206 (PPM writer); src/m09_png/yuv2rgb_png.c:122-164 (CRC-32, chunks, Adler-32) and
+ * :208-364 (PNG writer: filter 0, zlib stored blocks of <= 65535 bytes, one IDAT). */
+
+/* reference yuv2rgb_ppm.c:19-42 (libwebp VP8YuvToRgb, 14-bit fixed point, clip of v >> 6) */
+static inline uint8_t or_clip6(int v) { return (uint8_t)(v < 0 ? 0 : (v >> 6 > 255 ? 255 : v >> 6)); }
+static void or_yuv_rgb(int y, int u, int v, uint8_t* d) {
+	const int yy = (y * 19077) >> 8;
+	d[0] = or_clip6(yy + ((v * 26149) >> 8) - 14234);
+	d[1] = or_clip6(yy - ((u * 6419) >> 8) - ((v * 13320) >> 8) + 8708);
+	d[2] = or_clip6(yy + ((u * 33050) >> 8) - 17685);
+}
+
+/* Chroma value of output pixel (x, y) in plane p (stride s, cw x ch samples), reference
+ * yuv2rgb_ppm.c:44-121 + row pairing :178-202: row 0 uses chroma row 0 twice; row y >= 1 sits
+ * between chroma rows a = (y-1)/2 and b = min(a+1, ch-1), nearer a when y is odd.  Columns:
+ * x = 0 and (even width) x = w-1 use one chroma column (3:1 vertical blend); inner pixels pair
+ * up as (2k-1, 2k) between columns k-1 and k (9:3:3:1 with libwebp's two-step rounding). */
+static int or_chroma(const uint8_t* p, uint32_t s, uint32_t w, uint32_t ch, uint32_t x, uint32_t y) {
+	const uint32_t a = y ? (y - 1) >> 1 : 0, b = y ? ((a + 1 < ch) ? a + 1 : ch - 1) : 0;
+	const int near_a = (y == 0) || (y & 1);
+	const uint8_t* ra = p + (size_t)a * s;
+	const uint8_t* rb = p + (size_t)b * s;
+	if (x == 0 || ((w & 1) == 0 && x == w - 1)) {
+		const uint32_t c = x >> 1;
+		const int n = near_a ? ra[c] : rb[c], f = near_a ? rb[c] : ra[c];
+		return (3 * n + f + 2) >> 2;
+	}
+	const uint32_t k = (x + 1) >> 1; /* pair (2k-1, 2k): columns k-1, k */
+	const int tl = ra[k - 1], t = ra[k], l = rb[k - 1], u = rb[k];
+	const int avg = tl + t + l + u + 8;
+	const int d12 = (avg + 2 * (t + l)) >> 3, d03 = (avg + 2 * (tl + u)) >> 3;
+	if (near_a) return (x & 1) ? (d12 + tl) >> 1 : (d03 + t) >> 1;
+	return (x & 1) ? (d03 + l) >> 1 : (d12 + u) >> 1;
+}
+
+void oracle_rgb_row(const Yuv420Image* img, uint32_t y, uint8_t* dst) {
+	const uint32_t ch = (img->height + 1u) >> 1;
+	for (uint32_t x = 0; x < img->width; x++)
+		or_yuv_rgb(img->y[(size_t)y * img->stride_y + x], or_chroma(img->u, img->stride_uv, img->width, ch, x, y),
+		           or_chroma(img->v, img->stride_uv, img->width, ch, x, y), dst + 3 * (size_t)x);
+}
+
+static int or_ppm_header(uint32_t w, uint32_t h, char* hdr) { return sprintf(hdr, "P6\n%u %u\n255\n", w, h); }
+
+size_t oracle_ppm_size(uint32_t w, uint32_t h) {
+	char hdr[64];
+	return (size_t)or_ppm_header(w, h, hdr) + (size_t)w * h * 3u;
+}
+
+/* reference yuv2rgb_ppm.c:123-206: "P6\n<w> <h>\n255\n" + RGB rows */
+long oracle_ppm(const Yuv420Image* img, uint8_t* out, size_t cap) {
+	if (!img || !img->y || !img->u || !img->v || img->width == 0 || img->height == 0) return -1;
+	char hdr[64];
+	const int n = or_ppm_header(img->width, img->height, hdr);
+	const size_t total = (size_t)n + (size_t)img->width * img->height * 3u;
+	if (cap < total) return -1;
+	memcpy(out, hdr, (size_t)n);
+	for (uint32_t y = 0; y < img->height; y++) oracle_rgb_row(img, y, out + n + (size_t)y * img->width * 3u);
+	return (long)total;
+}
+
+/* reference yuv2rgb_png.c:122-133 (bitwise CRC-32, reflected 0xEDB88320) */
+static uint32_t or_crc32(uint32_t crc, const uint8_t* p, size_t n) {
+	crc = ~crc;
+	for (size_t i = 0; i < n; i++) {
+		crc ^= p[i];
+		for (int k = 0; k < 8; k++) crc = (crc & 1u) ? (0xEDB88320u ^ (crc >> 1)) : (crc >> 1);
+	}
+	return ~crc;
+}
+static void or_be32(uint8_t* p, uint32_t v) {
+	p[0] = (uint8_t)(v >> 24), p[1] = (uint8_t)(v >> 16), p[2] = (uint8_t)(v >> 8), p[3] = (uint8_t)v;
+}
+
+size_t oracle_png_size(uint32_t w, uint32_t h) {
+	const uint64_t raw = (uint64_t)h * (1u + 3ull * w);
+	const uint64_t blocks = (raw + 65534u) / 65535u;
+	return (size_t)(8 + 25 + 12 + (2 + raw + 5 * blocks + 4) + 12);
+}
+
+/* reference yuv2rgb_png.c:208-364: signature, IHDR (8-bit RGB), one IDAT holding a zlib stream
+ * (0x78 0x01, stored blocks of min(65535, rest) bytes of filter-0 scanlines, Adler-32), IEND */
+long oracle_png(const Yuv420Image* img, uint8_t* out, size_t cap) {
+	if (!img || !img->y || !img->u || !img->v || img->width == 0 || img->height == 0) return -1;
+	const uint32_t w = img->width, h = img->height, sb = 1u + 3u * w;
+	const uint64_t raw = (uint64_t)h * sb;
+	if (raw > 0x7FFFFFFFu) return -1;
+	const size_t total = oracle_png_size(w, h);
+	if (cap < total) return -1;
+	static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', 0x0D, 0x0A, 0x1A, 0x0A};
+	uint8_t* o = out;
+	memcpy(o, sig, 8), o += 8;
+	or_be32(o, 13), memcpy(o + 4, "IHDR", 4);
+	or_be32(o + 8, w), or_be32(o + 12, h);
+	o[16] = 8, o[17] = 2, o[18] = 0, o[19] = 0, o[20] = 0;
+	or_be32(o + 21, or_crc32(0, o + 4, 17)), o += 25;
+	const uint64_t blocks = (raw + 65534u) / 65535u, zlen = 2 + raw + 5 * blocks + 4;
+	uint8_t* idat = o;
+	or_be32(o, (uint32_t)zlen), memcpy(o + 4, "IDAT", 4), o += 8;
+	*o++ = 0x78, *o++ = 0x01;
+	uint8_t* line = (uint8_t*)malloc(sb);
+	if (!line) return -1;
+	uint32_t a = 1, b = 0, y = 0, pos = sb; /* pos: next byte of `line` (sb = exhausted) */
+	for (uint64_t left = raw; left > 0;) {
+		const uint32_t len = left > 65535u ? 65535u : (uint32_t)left;
+		*o++ = left <= 65535u ? 1 : 0;
+		*o++ = (uint8_t)len, *o++ = (uint8_t)(len >> 8);
+		*o++ = (uint8_t)~len, *o++ = (uint8_t)(~len >> 8);
+		for (uint32_t i = 0; i < len; i++) {
+			if (pos == sb) {
+				line[0] = 0;
+				oracle_rgb_row(img, y++, line + 1);
+				pos = 0;
+			}
+			const uint8_t c = line[pos++];
+			*o++ = c;
+			a = (a + c) % 65521u; /* reference yuv2rgb_png.c:150-164 */
+			b = (b + a) % 65521u;
+		}
+		left -= len;
+	}
+	free(line);
+	or_be32(o, (b << 16) | a), o += 4;
+	or_be32(o, or_crc32(0, idat + 4, (size_t)(o - idat - 4))), o += 4;
+	static const uint8_t iend[12] = {0, 0, 0, 0, 'I', 'E', 'N', 'D', 0xAE, 0x42, 0x60, 0x82};
+	memcpy(o, iend, 12), o += 12;
+	return (long)(o - out);
 }

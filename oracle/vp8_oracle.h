@@ -2,7 +2,7 @@
  * vp8_oracle.h -- TEST INFRASTRUCTURE ONLY.
  *
  * CPU restatement of the reference hot path (src/m06_recon/vp8_recon.c + src/m07_loopfilter/
- * vp8_loopfilter.c), used as the parity checker by tests/, __graft_entry__.smoke() and the
+ * vp8_loopfilter.c) and of the next stage, m08/m09 (YUV->RGB, PPM/PNG writers), used as the parity checker by tests/, __graft_entry__.smoke() and the
  * cpu_baseline leg of bench.py.  The product path (libvp8g.so) never links or calls it.
  *
  * Pinned by: tests/golden/manifest.json (sha256 of the reference decoder's own -yuv/-yuvf output
@@ -38,6 +38,15 @@ int oracle_reconstruct_i420(const Vp8KeyFrameHeader* kf, const Vp8DecodedFrame* 
  * per task; returns elapsed seconds (wall), or < 0 on error. */
 double oracle_time_batch(const Vp8KeyFrameHeader* const* kfs, const Vp8DecodedFrame* const* frames, int nframes, int n,
                          int threads, int filtered);
+
+/* m08 / m09 (reference src/m08_yuv2rgb_ppm/yuv2rgb_ppm.c, src/m09_png/yuv2rgb_png.c): one RGB24
+ * row of the fancy-upsampled conversion, and the complete PPM / PNG files the reference's
+ * yuv420_write_ppm_fd / yuv420_write_png_fd emit, written to memory (byte count, or -1). */
+void oracle_rgb_row(const Yuv420Image* img, uint32_t y, uint8_t* dst);
+size_t oracle_ppm_size(uint32_t w, uint32_t h);
+size_t oracle_png_size(uint32_t w, uint32_t h);
+long oracle_ppm(const Yuv420Image* img, uint8_t* out, size_t cap);
+long oracle_png(const Yuv420Image* img, uint8_t* out, size_t cap);
 
 #ifdef __cplusplus
 }

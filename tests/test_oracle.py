@@ -28,7 +28,7 @@ def test_manifest_covers_reference_corpus(manifest):
     assert sum(1 for k in files if k.split("/")[0] in ("webp", "testimages", "generated")) == 429
     assert sum(1 for k in files if k.startswith("commons/")) == 4
     assert sum(1 for k in files if k.startswith("big/")) == 8
-    assert manifest["libwebp_agreement"] == {"yuv": "441/441", "yuvf": "441/441"}
+    assert manifest["libwebp_agreement"] == {"yuv": "441/441", "yuvf": "441/441", "rgb": "441/441", "png_out": "90/90"}
 
 
 def test_oracle_and_front_end_vs_manifest(vp8g, manifest):
@@ -41,6 +41,21 @@ def test_oracle_and_front_end_vs_manifest(vp8g, manifest):
         for filt, key in ((False, "yuv_sha256"), (True, "yuvf_sha256")):
             if sha(vp8g.oracle_reconstruct(f, filt)) != ent[key]:
                 bad.append((rel, key))
+        f.free()
+    assert not bad, bad[:10]
+
+
+def test_oracle_ppm_png_vs_manifest(vp8g, manifest):
+    """m08/m09 restatement (YUV->RGB fancy upsampling, PPM and PNG writers) vs sha256 of the
+    reference decoder's own -ppm / -png files on every fixture (manifest: those equal libwebp's RGB
+    on all 441 files and the pixels of the reference's 90 dwebp PNG goldens)."""
+    bad = []
+    for rel, ent in sorted(manifest["files"].items()):
+        f = vp8g.decode_file(FIXTURES / rel)
+        i420 = vp8g.oracle_reconstruct(f, True)
+        for fmt in ("ppm", "png"):
+            if sha(vp8g.oracle_encode(i420, f.width, f.height, fmt)) != ent[fmt + "_sha256"]:
+                bad.append((rel, fmt))
         f.free()
     assert not bad, bad[:10]
 

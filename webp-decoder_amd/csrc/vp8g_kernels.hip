@@ -469,7 +469,7 @@ struct Pref {
 // workgroup of 12 or 16 waves per CU for batches smaller than the CU count (pick_waves).  Either
 // way at most 4 waves per SIMD, i.e. the full 128-VGPR budget.
 template <int NW>
-constexpr int min_waves_per_simd() { return NW >= 8 ? 4 : (NW >= 2 ? (2 * NW) / 4 : 1); }
+constexpr int min_waves_per_simd() { return NW == 10 ? 5 : (NW >= 8 ? 4 : (NW >= 2 ? (2 * NW) / 4 : 1)); }
 
 // Split mode (kS, small batches): a frame's MB row pairs are dealt over `nsplit` workgroups
 // ("parts") of NW waves each -- global wave g = part * NW + wave owns pairs g, g + nsplit*NW, ...
@@ -1163,7 +1163,11 @@ int device_cus() {
 }
 
 uint32_t pick_waves(uint32_t waves_hint, uint32_t max_mb_rows, uint32_t n_frames) {
+#ifdef VP8G_NW10  // diagnostic: 10 waves per frame at 5 waves per SIMD (needs the global context)
+	static const uint32_t kSupported[] = {1, 2, 4, 8, 10, 12, 16};
+#else
 	static const uint32_t kSupported[] = {1, 2, 4, 8, 12, 16};
+#endif
 	// default: 8 waves (two frames per CU) when the batch fills the chip; a batch with at most
 	// one frame per CU gets 16 waves per frame instead (twice the MB row pairs in flight)
 	const int n_cus = device_cus();
@@ -1209,6 +1213,9 @@ hipError_t launch_frames(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const 
 		VP8G_CASE(4)
 		VP8G_CASE(8)
 		VP8G_CASE(12)
+#ifdef VP8G_NW10
+		VP8G_CASE(10)
+#endif
 		default:
 		VP8G_CASE(16)
 	}

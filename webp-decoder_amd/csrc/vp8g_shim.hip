@@ -195,7 +195,11 @@ int run_locked(const std::vector<Vp8gFrameDesc>& descs, const Vp8gBatchArrays& a
 	uint32_t nw = vp8g::pick_waves(waves_hint, max_rows, n);
 	if ((may_split || env > 1) && env != 1 && !waves_hint && vp8g::pick_split(env, n, 8, max_rows) > 1) nw = 8;
 	uint8_t* gctx = nullptr;
+#ifdef VP8G_FORCE_GCTX  // diagnostic: per-column context in device memory for every frame
+	const bool big = true;
+#else
 	const bool big = vp8g::lds_bytes((int)nw, max_cols, false) > (size_t)vp8g::kMaxLds;
+#endif
 	if (big) {
 		const size_t need = descs.size() * (size_t)max_cols * vp8g::kCtxBytesPerCol;
 		HIP_TRY(grow(&g_dev.gctx, &g_dev.gctx_cap, need), "hipMalloc(ctx)");

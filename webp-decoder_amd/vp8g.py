@@ -294,8 +294,42 @@ def oracle_lib():
         lib.oracle_loopfilter.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, P(Vp8DecodedFrame)]
         lib.oracle_time_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int]
         lib.oracle_time_batch.restype = C.c_double
+        lib.oracle_ppm_size.argtypes = [C.c_uint32, C.c_uint32]
+        lib.oracle_ppm_size.restype = C.c_size_t
+        lib.oracle_png_size.argtypes = [C.c_uint32, C.c_uint32]
+        lib.oracle_png_size.restype = C.c_size_t
+        lib.oracle_ppm.argtypes = [P(Yuv420Image), C.c_void_p, C.c_size_t]
+        lib.oracle_ppm.restype = C.c_long
+        lib.oracle_png.argtypes = [P(Yuv420Image), C.c_void_p, C.c_size_t]
+        lib.oracle_png.restype = C.c_long
         lib._typed = True
     return lib
+
+
+def image_from_i420(buf: bytes, w: int, h: int):
+    """A Yuv420Image view of cropped I420 bytes (Y w*h, U, V each ceil(w/2)*ceil(h/2)); the
+    returned numpy array keeps the memory alive."""
+    a = np.frombuffer(buf, dtype=np.uint8).copy()
+    cw, ch = (w + 1) // 2, (h + 1) // 2
+    img = Yuv420Image(w, h, w, cw)
+    base = a.ctypes.data
+    img.y = C.cast(base, C.POINTER(C.c_uint8))
+    img.u = C.cast(base + w * h, C.POINTER(C.c_uint8))
+    img.v = C.cast(base + w * h + cw * ch, C.POINTER(C.c_uint8))
+    return img, a
+
+
+def oracle_encode(i420: bytes, w: int, h: int, fmt: str) -> bytes:
+    """m08/m09 restatement: the PPM ("ppm") or PNG ("png") file of a cropped I420 image."""
+    lib = oracle_lib()
+    img, keep = image_from_i420(i420, w, h)
+    n = (lib.oracle_ppm_size if fmt == "ppm" else lib.oracle_png_size)(w, h)
+    out = np.empty(n, dtype=np.uint8)
+    got = (lib.oracle_ppm if fmt == "ppm" else lib.oracle_png)(C.byref(img), out.ctypes.data, n)
+    del keep
+    if got != n:
+        raise RuntimeError(f"oracle {fmt} failed ({got} of {n})")
+    return out.tobytes()
 
 
 def oracle_reconstruct(f: Frame, filtered: bool) -> bytes:
