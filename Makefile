@@ -15,7 +15,7 @@ OFFLOAD_ARCH ?= gfx950
 
 HOST_SRC := $(PKG)/host/webp_riff.c $(PKG)/host/vp8_parse.c $(PKG)/host/vp8_synth.c
 HOST_HDR := $(PKG)/host/vp8_front.h $(PKG)/host/vp8_bool.h $(PKG)/host/vp8_tables.inc include/vp8g.h
-HIP_SRC := $(PKG)/csrc/vp8g_kernels.hip $(PKG)/csrc/vp8g_shim.hip
+HIP_SRC := $(PKG)/csrc/vp8g_kernels.hip $(PKG)/csrc/vp8g_shim.hip $(PKG)/csrc/vp8g_rgb.hip
 HIP_HDR := $(PKG)/csrc/vp8g_device.h include/vp8g.h
 
 CFLAGS := -std=c11 -O3 -march=x86-64-v3 -Wall -Wextra -Wpedantic -fPIC -D_POSIX_C_SOURCE=200809L

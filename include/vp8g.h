@@ -207,11 +207,68 @@ int vp8g_decode_batch_device(const Vp8gFrameDesc* h_descs, const Vp8gFrameDesc* 
 int vp8g_reconstruct_batch(const Vp8KeyFrameHeader* const* kfs, const Vp8DecodedFrame* const* frames, uint32_t n,
                            int filtered, Yuv420Image* outs);
 
+/* ---- m08 / m09 boundary: I420 -> RGB24 ("fancy" 4:2:0 upsampling) and the file writers -- */
+
+/* replaces src/m08_yuv2rgb_ppm/yuv2rgb_ppm.c:123 (decl yuv2rgb_ppm.h:10): binary PPM (P6) of img
+ * to fd, full-range Rec.601 as libwebp's VP8YuvToRgb.  0, or -1 + errno (EINVAL bad arguments or
+ * zero size, ENOMEM, EIO on a HIP failure, or write(2)'s errno). */
+int yuv420_write_ppm_fd(int fd, const Yuv420Image* img);
+
+/* replaces src/m09_png/yuv2rgb_png.c:208 (decl yuv2rgb_png.h:10): 8-bit RGB PNG, filter 0 on every
+ * scanline, one IDAT holding a zlib stream of stored blocks (<= 65535 bytes each); EFBIG when the
+ * raw scanline stream exceeds 2^31 - 1 bytes.  Same errors as yuv420_write_ppm_fd otherwise. */
+int yuv420_write_png_fd(int fd, const Yuv420Image* img);
+
+#define VP8G_ENC_RGB 0u /* RGB24 rows, no header: w*h*3 bytes */
+#define VP8G_ENC_PPM 1u /* the file yuv420_write_ppm_fd writes */
+#define VP8G_ENC_PNG 2u /* the file yuv420_write_png_fd writes */
+#define VP8G_ENC_SPAN 32768u /* output bytes per workgroup task */
+
+/* Per-image descriptor of the encoder kernels (built by vp8g_make_enc_desc).  1432 bytes. */
+typedef struct {
+	uint32_t width, height;
+	uint32_t stride_y, stride_uv;  /* source plane strides */
+	uint64_t src_y, src_u, src_v;  /* byte offsets of the source planes in the source buffer */
+	uint64_t out;                  /* byte offset of the file in the output buffer (16-B aligned) */
+	uint64_t file_len;             /* bytes of the file */
+	uint32_t format;               /* VP8G_ENC_* */
+	uint32_t prefix_len;           /* bytes before the first pixel byte (PNG: signature, IHDR, IDAT
+	                                  header, zlib header = 43) */
+	uint32_t row_bytes;            /* bytes per row of the pixel stream (3w; PNG 1 + 3w) */
+	uint32_t raw_len;              /* pixel stream bytes (height * row_bytes) */
+	uint32_t span0, nspans;        /* this image's VP8G_ENC_SPAN-byte tasks in the launch */
+	uint32_t zend;                 /* PNG: file offset just past the zlib stream (Adler-32 ends here) */
+	uint32_t crc_init;             /* PNG: CRC-32 correction for the 0xFFFFFFFF initial value */
+	uint8_t prefix[48];
+	uint32_t reserved[4];
+	uint32_t crc_ops[10][32];      /* PNG: GF(2) operators (columns) of the checksum combine */
+} Vp8gEncDesc;
+
+/* Fill the descriptor of one w x h image whose planes sit at src_* (strides stride_*) in the
+ * source buffer, encoded as `format` at out_offset (16-B aligned) of the output buffer; its tasks
+ * start at span0.  Returns the image's task count (> 0), or 0 + errno (EINVAL, EFBIG). */
+uint32_t vp8g_make_enc_desc(uint32_t width, uint32_t height, uint32_t format, uint64_t src_y, uint64_t src_u,
+                            uint64_t src_v, uint32_t stride_y, uint32_t stride_uv, uint64_t out_offset,
+                            uint32_t span0, Vp8gEncDesc* out);
+
+/* Encoded file size (0 for a bad format / size). */
+uint64_t vp8g_encoded_size(uint32_t format, uint32_t width, uint32_t height);
+
+/* Device workspace bytes for a launch of `total_spans` tasks. */
+uint64_t vp8g_encode_workspace_size(uint32_t total_spans);
+
+/* Encode n images (device-resident source planes -> files in d_out) on `hip_stream`: one launch
+ * over all tasks (pixels, layout, per-task checksum partials) plus, when some image is a PNG, one
+ * that finishes the Adler-32 / CRC-32 fields.  h_descs / d_descs: host and device copies of the
+ * descriptors; d_work: vp8g_encode_workspace_size() bytes.  Asynchronous; 0 or -1 + errno. */
+int vp8g_encode_batch_device(const Vp8gEncDesc* h_descs, const Vp8gEncDesc* d_descs, uint32_t n, const uint8_t* d_src,
+                             uint8_t* d_out, uint8_t* d_work, void* hip_stream);
+
 /* Name of the last HIP error seen by this library in the calling thread ("" if none). */
 const char* vp8g_last_error(void);
 
 /* ABI version of this header (bumped on any layout change). */
-#define VP8G_ABI_VERSION 1
+#define VP8G_ABI_VERSION 2
 uint32_t vp8g_abi_version(void);
 
 #ifdef __cplusplus

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol(vp8g):
     lib = vp8g.gpu_lib()
     missing = [f for f in header_functions() if not hasattr(lib, f)]
     assert not missing, missing
-    assert lib.vp8g_abi_version() == 1
+    assert lib.vp8g_abi_version() == 2
 
 
 def test_struct_layouts(vp8g):
@@ -155,3 +155,59 @@ def test_cli_info_reports_reference_hash(manifest):
     r = subprocess.run([str(DECODER), "-info", str(FIXTURES / rel)], capture_output=True, text=True)
     assert r.returncode == 0
     assert manifest["files"][rel]["coeff_hash"] in r.stdout
+
+
+def _raw_crc(r, data):  # CRC-32 register update without conditioning (init r, no final xor)
+    import zlib
+    return zlib.crc32(data, r ^ 0xFFFFFFFF) ^ 0xFFFFFFFF
+
+
+def _op(cols, v):
+    r = 0
+    for i in range(32):
+        if (v >> i) & 1:
+            r ^= cols[i]
+    return r
+
+
+@pytest.mark.parametrize("w,h", [(1, 1), (333, 97), (21845, 2), (1024, 700)])
+def test_png_descriptor_and_checksum_algebra(vp8g, w, h):
+    """Host side of the device PNG writer: vp8g_make_enc_desc's layout (prefix bytes, sizes) equals
+    the oracle's file, and its GF(2) CRC operators -- replayed here exactly as the finishing kernel
+    combines per-task CRCs (Horner over each thread's tasks, tree, un-pad, Adler patch, init) --
+    give the file's IDAT CRC and Adler-32.  No GPU involved."""
+    import struct
+    import zlib
+    rng = np.random.default_rng(w + h)
+    i420 = rng.integers(0, 256, size=w * h + 2 * ((w + 1) // 2) * ((h + 1) // 2), dtype=np.uint8).tobytes()
+    png = vp8g.oracle_encode(i420, w, h, "png")
+    d = vp8g.Vp8gEncDesc()
+    lib = vp8g.gpu_lib()
+    S = vp8g.ENC_SPAN
+    G = lib.vp8g_make_enc_desc(w, h, 2, 0, 0, 0, w, (w + 1) // 2, 0, 0, C.byref(d))
+    assert G == (len(png) + S - 1) // S and d.file_len == len(png) == lib.vp8g_encoded_size(2, w, h)
+    assert bytes(d.prefix[:d.prefix_len]) == png[:d.prefix_len]
+    E = d.zend
+    # per-task raw CRCs over the task's bytes, everything outside [37, E-4) read as zero
+    buf = bytearray(G * S)
+    buf[37:E - 4] = png[37:E - 4]
+    parts = [_raw_crc(0, bytes(buf[g * S:(g + 1) * S])) for g in range(G)]
+    m = (G + 255) // 256
+    pad = 256 * m - G
+    ops = [list(d.crc_ops[i]) for i in range(10)]
+    acc = []
+    for t in range(256):
+        c = 0
+        for i in range(m):
+            gi = t * m + i - pad
+            c = _op(ops[0], c) ^ (parts[gi] if gi >= 0 else 0)
+        acc.append(c)
+    for lvl in range(8):
+        for t in range(256 >> (lvl + 1)):
+            lo, hi = t << (lvl + 1), (t << (lvl + 1)) + (1 << lvl)
+            acc[lo] = _op(ops[1 + lvl], acc[lo]) ^ acc[hi]
+    adler = png[E - 4:E]
+    crc = (_op(ops[9], acc[0]) ^ _raw_crc(0, adler) ^ d.crc_init) ^ 0xFFFFFFFF
+    assert crc == struct.unpack(">I", png[E:E + 4])[0] == zlib.crc32(png[37:E])
+    raw = zlib.decompress(png[41:E])
+    assert struct.unpack(">I", adler)[0] == zlib.adler32(raw)

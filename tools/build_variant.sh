@@ -3,4 +3,4 @@
 OUT=$1; shift
 /opt/rocm/bin/hipcc -std=c++17 -O3 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-function -fvisibility=hidden \
   -I include -munsafe-fp-atomics "$@" -shared -Wl,-Bsymbolic -o "$OUT" \
-  webp-decoder_amd/csrc/vp8g_kernels.hip webp-decoder_amd/csrc/vp8g_shim.hip -lpthread
+  webp-decoder_amd/csrc/vp8g_kernels.hip webp-decoder_amd/csrc/vp8g_shim.hip webp-decoder_amd/csrc/vp8g_rgb.hip -lpthread

@@ -65,4 +65,7 @@ uint32_t pick_split(uint32_t split_hint, uint32_t n_frames, uint32_t nw, uint32_
 // waves_hint if non-zero, else 8, or 16 when n_frames <= the device's CU count.
 uint32_t pick_waves(uint32_t waves_hint, uint32_t max_mb_rows, uint32_t n_frames);
 
+// Record a HIP failure for vp8g_last_error() (calling thread).
+void set_error_text(const char* where, hipError_t e);
+
 }  // namespace vp8g

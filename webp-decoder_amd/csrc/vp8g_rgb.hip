@@ -1,0 +1,646 @@
+// vp8g_rgb.hip -- m08 / m09 on the GPU: "fancy" 4:2:0 upsampled I420 -> RGB24 and the exact
+// PPM / PNG files the reference writes (src/m08_yuv2rgb_ppm/yuv2rgb_ppm.c, src/m09_png/yuv2rgb_png.c).
+//
+// The output FILE is the unit of work: it is cut into VP8G_ENC_SPAN-byte spans, one workgroup
+// task each (a workgroup loops over tasks).  A task
+//   1. computes the pixel bytes that land in its span (one thread per horizontal pixel pair: the
+//      pair shares its four chroma samples and the 9:3:3:1 diagonals) and the few layout bytes
+//      (PPM header; PNG signature / IHDR / IDAT header / zlib header, the 5-byte stored-block
+//      headers, the IEND trailer) into an LDS image of the span;
+//   2. streams the span to HBM as 16-byte stores, 128 contiguous bytes per thread, and -- PNG --
+//      folds the same bytes into a CRC-32 (slice-by-4 tables) and Adler-32 partial sums;
+//   3. combines the 256 thread CRCs with GF(2) shift operators (nibble tables in LDS) into one
+//      CRC per span, written with the span's Adler partials to the workspace.
+// A second, small launch (one workgroup per PNG) combines the span partials and writes the
+// Adler-32 and the IDAT CRC.  Every byte of every file is produced on the device.
+//
+// CRC algebra (reflected CRC-32, polynomial 0xEDB88320): the raw register update is linear, so
+// with Z_n = "feed n zero bytes", crc_raw(A || B) = Z_|B|(crc_raw(A)) ^ crc_raw(B), leading zero
+// bytes change nothing, and crc32(M) = ~(crc_raw(M) ^ Z_|M|(0xFFFFFFFF)).  Spans are CRC'd over
+// the whole span with every byte outside the IDAT CRC range (and the 4 Adler bytes, patched in at
+// the end) read as zero; the padded total is shifted back by Z_-d.  The host precomputes the
+// operators (32 columns each).
+#include <errno.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#include <map>
+#include <mutex>
+#include <tuple>
+#include <vector>
+
+#include "vp8g_device.h"
+
+#define VP8G_API extern "C" __attribute__((visibility("default")))
+#define DEV __device__ __forceinline__
+
+namespace {
+
+constexpr uint32_t kSpan = VP8G_ENC_SPAN;
+constexpr int kThreads = 256;
+constexpr uint32_t kPerThread = kSpan / kThreads;  // 128 contiguous file bytes per thread
+constexpr uint32_t kMod = 65521u;                  // Adler-32
+constexpr uint32_t kBlk = 65535u;                  // stored-deflate block payload
+constexpr uint32_t kBlkFile = kBlk + 5u;           // ... plus its header
+constexpr uint32_t kPngPrefix = 43u;               // signature 8, IHDR 25, IDAT len/type 8, zlib 2
+constexpr uint32_t kPngRaw0 = kPngPrefix + 5u;     // file offset of the first pixel-stream byte
+constexpr uint32_t kCrcStart = 37u;                // IDAT CRC covers the chunk type + data
+constexpr int kTreeLevels = 8;                     // log2(kThreads)
+static_assert(kSpan % kThreads == 0 && kPerThread % 16 == 0, "span layout");
+
+// Tables shared by every task (8 KB): CRC-32 slice-by-4 tables T0..T3, then for the in-span tree
+// the nibble tables of Z_{128 * 2^l}, l = 0..7: tab[l][j][v] = Z(v << 4j).
+constexpr int kTabWords = 4 * 256 + kTreeLevels * 8 * 16;
+
+struct EncLds {
+	uint8_t buf[kSpan];
+	uint32_t tab[kTabWords];
+	uint32_t red[3][kThreads];
+};
+
+// ---- device helpers ----------------------------------------------------------------------
+// reference yuv2rgb_ppm.c:19-42: libwebp VP8YuvToRgb (14-bit fixed point, clip of v >> 6)
+DEV uint32_t clip6(int v) { return (uint32_t)min(max(v >> 6, 0), 255); }
+DEV uint32_t yuv_rgb(int y, int u, int v) {  // packed r | g << 8 | b << 16
+	const int yy = (y * 19077) >> 8;
+	const uint32_t r = clip6(yy + ((v * 26149) >> 8) - 14234);
+	const uint32_t g = clip6(yy - ((u * 6419) >> 8) - ((v * 13320) >> 8) + 8708);
+	const uint32_t b = clip6(yy + ((u * 33050) >> 8) - 17685);
+	return r | (g << 8) | (b << 16);
+}
+
+// file offset of pixel-stream byte p (PNG: stored blocks of kBlk bytes behind 5-byte headers)
+DEV uint32_t png_file_of_raw(uint32_t p) { return kPngRaw0 + p + 5u * (p / kBlk); }
+// first pixel-stream byte at or after file offset q, clamped to n
+DEV uint32_t raw_of_file(const Vp8gEncDesc& d, uint32_t q) {
+	if (d.format != VP8G_ENC_PNG) return q <= d.prefix_len ? 0u : min(q - d.prefix_len, d.raw_len);
+	if (q <= kPngRaw0) return 0u;
+	const uint32_t z = q - kPngPrefix, k = z / kBlkFile, o = z - k * kBlkFile;
+	return min(k * kBlk + (o < 5u ? 0u : o - 5u), d.raw_len);
+}
+
+DEV uint32_t crc_byte(const uint32_t* t0, uint32_t c, uint32_t b) { return t0[(c ^ b) & 255u] ^ (c >> 8); }
+DEV uint32_t crc_word(const uint32_t* t, uint32_t c, uint32_t w) {  // slice-by-4 (little-endian word)
+	c ^= w;
+	return t[768 + (c & 255u)] ^ t[512 + ((c >> 8) & 255u)] ^ t[256 + ((c >> 16) & 255u)] ^ t[c >> 24];
+}
+DEV uint32_t nib_apply(const uint32_t* nt, uint32_t v) {  // GF(2) operator via 8 nibble tables
+	uint32_t r = 0;
+#pragma unroll
+	for (int j = 0; j < 8; j++) r ^= nt[j * 16 + ((v >> (4 * j)) & 15u)];
+	return r;
+}
+DEV uint32_t op_apply(const uint32_t* col, uint32_t v) {  // GF(2) operator by columns
+	uint32_t r = 0;
+#pragma unroll
+	for (int i = 0; i < 32; i++) r ^= ((v >> i) & 1u) ? col[i] : 0u;
+	return r;
+}
+
+// ---- task kernel -------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void enc_kernel(const Vp8gEncDesc* __restrict__ D, uint32_t n, uint32_t total,
+                                                       const uint8_t* __restrict__ src, uint8_t* __restrict__ out,
+                                                       uint32_t* __restrict__ part, const uint32_t* __restrict__ tables) {
+	__shared__ EncLds L;
+	const uint32_t tid = threadIdx.x;
+	for (uint32_t i = tid; i < (uint32_t)kTabWords; i += kThreads) L.tab[i] = tables[i];
+	uint32_t img = 0;
+	for (uint32_t g = blockIdx.x; g < total; g += gridDim.x) {
+		while (img + 1 < n && D[img + 1].span0 <= g) img++;  // tasks are numbered image by image
+		const Vp8gEncDesc& d = D[img];
+		const bool png = d.format == VP8G_ENC_PNG;
+		const uint32_t F0 = (g - d.span0) * kSpan;  // file offset of this span
+		const uint32_t flen = (uint32_t)d.file_len;
+		__syncthreads();  // the previous task's LDS readers are done (and the tables are loaded)
+
+		// -- 1a. pixel bytes of the span: one thread per unit k of a row = pixels {2k-1, 2k}
+		const uint32_t p_lo = raw_of_file(d, F0), p_hi = raw_of_file(d, F0 + kSpan);
+		if (p_lo < p_hi) {
+			const uint32_t W = d.width, H = d.height, SB = d.row_bytes, f = png ? 1u : 0u;
+			const uint32_t UPR = W / 2u + 1u, cw = (W + 1u) >> 1, ch = (H + 1u) >> 1;
+			const uint32_t ylo = p_lo / SB, rlo = p_lo - ylo * SB, xlo = rlo < f ? 0u : (rlo - f) / 3u;
+			const uint32_t yhi = (p_hi - 1u) / SB, rhi = p_hi - 1u - yhi * SB, xhi = rhi < f ? 0u : (rhi - f) / 3u;
+			const uint32_t gu0 = ylo * UPR + ((xlo + 1u) >> 1), gu1 = yhi * UPR + ((xhi + 1u) >> 1) + 1u;
+			const float inv = 1.0f / (float)UPR;
+			const uint8_t* Y = src + d.src_y;
+			const uint8_t* U = src + d.src_u;
+			const uint8_t* V = src + d.src_v;
+			for (uint32_t gu = gu0 + tid; gu < gu1; gu += kThreads) {
+				// (row, unit) = divmod(gu, UPR): float estimate, exact after the corrections
+				int y = (int)((float)gu * inv);
+				int k = (int)gu - y * (int)UPR;
+				while (k < 0) k += (int)UPR, y--;
+				while (k >= (int)UPR) k -= (int)UPR, y++;
+				// chroma rows (reference yuv2rgb_ppm.c:178-202): row 0 uses row 0 twice; row y
+				// sits between a = (y-1)/2 and b = min(a+1, ch-1), nearer a when y is odd
+				const uint32_t a = y ? (uint32_t)(y - 1) >> 1 : 0u, b = y ? min(a + 1u, ch - 1u) : 0u;
+				const bool near_a = y == 0 || (y & 1);
+				// columns (reference yuv2rgb_ppm.c:44-121): the pair (2k-1, 2k) blends columns k-1 and
+				// k; at the edges both are the same column, which gives the 3:1 edge formula exactly
+				const uint32_t cl = k ? (uint32_t)k - 1u : 0u, cr = min((uint32_t)k, cw - 1u);
+				const size_t ra = (size_t)a * d.stride_uv, rb = (size_t)b * d.stride_uv;
+				const int tlu = U[ra + cl], tu = U[ra + cr], lu = U[rb + cl], uu = U[rb + cr];
+				const int tlv = V[ra + cl], tv = V[ra + cr], lv = V[rb + cl], uv = V[rb + cr];
+				const int au = tlu + tu + lu + uu + 8, av = tlv + tv + lv + uv + 8;
+				const int d12u = (au + 2 * (tu + lu)) >> 3, d03u = (au + 2 * (tlu + uu)) >> 3;
+				const int d12v = (av + 2 * (tv + lv)) >> 3, d03v = (av + 2 * (tlv + uv)) >> 3;
+				const int u_odd = near_a ? (d12u + tlu) >> 1 : (d03u + lu) >> 1;
+				const int v_odd = near_a ? (d12v + tlv) >> 1 : (d03v + lv) >> 1;
+				const int u_even = near_a ? (d03u + tu) >> 1 : (d12u + uu) >> 1;
+				const int v_even = near_a ? (d03v + tv) >> 1 : (d12v + uv) >> 1;
+				const uint8_t* yr = Y + (size_t)y * d.stride_y;
+				const bool has_odd = k > 0, has_even = 2u * (uint32_t)k < W;
+				const uint32_t x_odd = 2u * (uint32_t)k - 1u, x_even = 2u * (uint32_t)k;
+				// (indices clamped so that no load is ever out of the plane, even if speculated)
+				const uint32_t c_odd = has_odd ? yuv_rgb(yr[has_odd ? x_odd : 0u], u_odd, v_odd) : 0u;
+				const uint32_t c_even = has_even ? yuv_rgb(yr[has_even ? x_even : x_odd], u_even, v_even) : 0u;
+				// bytes: [filter byte (PNG, k == 0)] [odd pixel] [even pixel], at raw offsets from p0
+				const uint32_t rowp = (uint32_t)y * SB;
+				const uint32_t pb = k ? rowp + f + 3u * x_odd : rowp;  // first byte this unit writes
+				const uint32_t nb = (k ? 0u : f) + (has_odd ? 3u : 0u) + (has_even ? 3u : 0u);
+				uint32_t qb, bnd = 0xFFFFFFFFu;
+				if (png) {
+					const uint32_t blk = pb / kBlk;
+					qb = kPngRaw0 + pb + 5u * blk;
+					bnd = (blk + 1u) * kBlk;  // raw offset where the next block header intervenes
+				} else {
+					qb = d.prefix_len + pb;
+				}
+				uint64_t bytes = k ? ((uint64_t)c_even << 24) | c_odd : (f ? ((uint64_t)c_even << 8) : (uint64_t)c_even);
+				for (uint32_t i = 0; i < nb; i++) {
+					const uint32_t q = qb + i + ((pb + i >= bnd) ? 5u : 0u) - F0;
+					if (q < kSpan) L.buf[q] = (uint8_t)(bytes >> (8 * i));
+				}
+			}
+		}
+		// -- 1b. layout bytes in the span
+		if (tid < 64) {
+			// prefix (PPM header / PNG signature + IHDR + IDAT header + zlib header)
+			if (tid < d.prefix_len && tid >= F0 && tid < F0 + kSpan) L.buf[tid - F0] = d.prefix[tid];
+		} else if (png && tid < 74) {
+			// stored-block headers: at most two blocks meet a span
+			const uint32_t j = tid - 64, kc = (F0 >= kPngPrefix ? (F0 - kPngPrefix) / kBlkFile : 0u) + j / 5u;
+			const uint32_t q = kPngPrefix + kc * kBlkFile + j % 5u;
+			const uint32_t nblk = (d.raw_len + kBlk - 1u) / kBlk;
+			if (kc < nblk && q >= F0 && q < F0 + kSpan) {
+				const uint32_t len = min(kBlk, d.raw_len - kc * kBlk);
+				const uint32_t hdr[5] = {kc + 1u == nblk ? 1u : 0u, len & 255u, len >> 8, ~len & 255u, (~len >> 8) & 255u};
+				L.buf[q - F0] = (uint8_t)hdr[j % 5u];
+			}
+		} else if (png && tid >= 96 && tid < 116) {
+			// Adler-32 and CRC placeholders (written by the finishing launch), IEND chunk
+			const uint32_t i = tid - 96, q = d.zend - 4u + i;
+			const uint8_t iend[12] = {0, 0, 0, 0, 'I', 'E', 'N', 'D', 0xAE, 0x42, 0x60, 0x82};
+			if (q >= F0 && q < F0 + kSpan) L.buf[q - F0] = i < 8 ? 0 : iend[i - 8];
+		} else if (tid >= 128 && tid < 144) {
+			// alignment padding after the file (the last 16-byte store covers it)
+			const uint32_t q = flen + (tid - 128);
+			if (q >= F0 && q < F0 + kSpan && q < ((flen + 15u) & ~15u)) L.buf[q - F0] = 0;
+		}
+		__syncthreads();
+
+		// -- 2. stream 128 contiguous bytes per thread to HBM (+ PNG checksum partials)
+		const uint32_t q0 = F0 + tid * kPerThread;
+		const uint32_t* bw = (const uint32_t*)(L.buf + tid * kPerThread);
+		uint8_t* dst = out + d.out + q0;
+#pragma unroll
+		for (uint32_t i = 0; i < kPerThread / 16u; i++)
+			if (q0 + 16u * i < flen) *(uint4*)(dst + 16u * i) = *(const uint4*)(bw + 4u * i);
+		if (png) {
+			uint32_t c = 0, s0 = 0, s1 = 0;
+			const uint32_t N = d.raw_len;
+			const uint32_t z0 = q0 - kPngPrefix, k0 = z0 / kBlkFile, o0 = z0 - k0 * kBlkFile;
+			const uint32_t p0 = k0 * kBlk + o0 - 5u;
+			const bool fast = q0 >= kPngRaw0 && o0 >= 5u && o0 + kPerThread <= kBlkFile && p0 + kPerThread <= N;
+			if (fast) {
+				// all 128 bytes are pixel-stream bytes of one stored block (inside the CRC range)
+				uint32_t sj = 0;
+#pragma unroll 8
+				for (uint32_t i = 0; i < kPerThread / 4u; i++) {
+					const uint32_t w = bw[i];
+					c = crc_word(L.tab, c, w);
+					s0 = __builtin_amdgcn_sad_u8(w, 0u, s0);
+					sj = __builtin_amdgcn_udot4(w, 0x03020100u + 0x04040404u * i, sj, false);
+				}
+				// Adler b-sum: sum over bytes of (N - p) r_p = (N - p0) s0 - sum j r_j (mod 65521)
+				const uint32_t w0 = (N - p0) % kMod;
+				s1 = ((w0 * s0) % kMod + kMod - sj % kMod) % kMod;
+				s0 %= kMod;
+			} else if (q0 < d.zend + 4u) {
+				const uint32_t crc_end = d.zend - 4u, raw_end = png_file_of_raw(N - 1u) + 1u;
+				for (uint32_t j = 0; j < kPerThread; j++) {
+					const uint32_t q = q0 + j, v = L.buf[tid * kPerThread + j];
+					c = crc_byte(L.tab, c, (q >= kCrcStart && q < crc_end) ? v : 0u);
+					if (q >= kPngRaw0 && q < raw_end) {
+						const uint32_t z = q - kPngPrefix, k = z / kBlkFile, o = z - k * kBlkFile;
+						if (o >= 5u) {
+							const uint32_t p = k * kBlk + o - 5u;
+							s0 = (s0 + v) % kMod;
+							s1 = (s1 + ((N - p) % kMod) * v) % kMod;
+						}
+					}
+				}
+			} else {
+				// past the CRC range: zero bytes (the padded tail of the last span)
+#pragma unroll 8
+				for (uint32_t i = 0; i < kPerThread / 4u; i++) c = crc_word(L.tab, c, 0u);
+			}
+			// -- 3. span CRC: tree over the 256 thread CRCs (each over 128 bytes)
+			L.red[0][tid] = c;
+			L.red[1][tid] = s0;
+			L.red[2][tid] = s1;
+			for (int l = 0; l < kTreeLevels; l++) {
+				__syncthreads();
+				if (tid < (uint32_t)(kThreads >> (l + 1))) {
+					const uint32_t lo = tid << (l + 1), hi = lo + (1u << l);
+					L.red[0][lo] = nib_apply(L.tab + 1024 + l * 128, L.red[0][lo]) ^ L.red[0][hi];
+					L.red[1][lo] = (L.red[1][lo] + L.red[1][hi]) % kMod;
+					L.red[2][lo] = (L.red[2][lo] + L.red[2][hi]) % kMod;
+				}
+			}
+			if (tid == 0) {
+				uint32_t* pp = part + 4u * g;
+				pp[0] = L.red[0][0];
+				pp[1] = L.red[1][0];
+				pp[2] = L.red[2][0];
+			}
+		}
+	}
+}
+
+// ---- PNG finishing kernel: one workgroup per image ---------------------------------------
+__global__ __launch_bounds__(kThreads) void png_finish_kernel(const Vp8gEncDesc* __restrict__ D,
+                                                              const uint32_t* __restrict__ part, uint8_t* __restrict__ out,
+                                                              const uint32_t* __restrict__ tables) {
+	__shared__ uint32_t red[3][kThreads];
+	const Vp8gEncDesc& d = D[blockIdx.x];
+	if (d.format != VP8G_ENC_PNG) return;
+	const uint32_t tid = threadIdx.x, G = d.nspans, m = (G + kThreads - 1u) / kThreads, pad = m * kThreads - G;
+	// Horner over this thread's m consecutive spans (front-padded with zero spans: neutral)
+	uint32_t c = 0, s0 = 0, s1 = 0;
+	for (uint32_t i = 0; i < m; i++) {
+		const int gi = (int)(tid * m + i) - (int)pad;
+		c = op_apply(d.crc_ops[0], c);
+		if (gi >= 0) {
+			const uint32_t* pp = part + 4u * (d.span0 + (uint32_t)gi);
+			c ^= pp[0];
+			s0 = (s0 + pp[1]) % kMod;
+			s1 = (s1 + pp[2]) % kMod;
+		}
+	}
+	red[0][tid] = c;
+	red[1][tid] = s0;
+	red[2][tid] = s1;
+	for (int l = 0; l < kTreeLevels; l++) {
+		__syncthreads();
+		if (tid < (uint32_t)(kThreads >> (l + 1))) {
+			const uint32_t lo = tid << (l + 1), hi = lo + (1u << l);
+			red[0][lo] = op_apply(d.crc_ops[1 + l], red[0][lo]) ^ red[0][hi];
+			red[1][lo] = (red[1][lo] + red[1][hi]) % kMod;
+			red[2][lo] = (red[2][lo] + red[2][hi]) % kMod;
+		}
+	}
+	__syncthreads();
+	if (tid == 0) {
+		const uint32_t a = (1u + red[1][0]) % kMod, b = (d.raw_len % kMod + red[2][0]) % kMod;
+		const uint32_t adler = (b << 16) | a;
+		const uint8_t ab[4] = {(uint8_t)(adler >> 24), (uint8_t)(adler >> 16), (uint8_t)(adler >> 8), (uint8_t)adler};
+		uint32_t craw = op_apply(d.crc_ops[9], red[0][0]);  // un-pad: Z_-d
+		uint32_t ca = 0;
+		for (int i = 0; i < 4; i++) ca = crc_byte(tables, ca, ab[i]);
+		const uint32_t crc = ~(craw ^ ca ^ d.crc_init);
+		uint8_t* f = out + d.out + d.zend - 4u;
+		for (int i = 0; i < 4; i++) f[i] = ab[i];
+		f[4] = (uint8_t)(crc >> 24), f[5] = (uint8_t)(crc >> 16), f[6] = (uint8_t)(crc >> 8), f[7] = (uint8_t)crc;
+	}
+}
+
+// ---- host: GF(2) operators of the CRC-32 register -----------------------------------------
+struct Op {
+	uint32_t c[32];
+};
+uint32_t op_host_apply(const Op& m, uint32_t v) {
+	uint32_t r = 0;
+	for (int i = 0; i < 32; i++)
+		if ((v >> i) & 1u) r ^= m.c[i];
+	return r;
+}
+Op op_mul(const Op& a, const Op& b) {  // a after b
+	Op r;
+	for (int i = 0; i < 32; i++) r.c[i] = op_host_apply(a, b.c[i]);
+	return r;
+}
+Op op_zero_byte() {
+	Op r;
+	for (int i = 0; i < 32; i++) {
+		uint32_t c = 1u << i;
+		for (int k = 0; k < 8; k++) c = (c & 1u) ? (c >> 1) ^ 0xEDB88320u : c >> 1;
+		r.c[i] = c;
+	}
+	return r;
+}
+Op op_identity() {
+	Op r;
+	for (int i = 0; i < 32; i++) r.c[i] = 1u << i;
+	return r;
+}
+Op op_zeros(uint64_t n) {  // Z_n
+	Op r = op_identity(), p = op_zero_byte();
+	for (; n; n >>= 1, p = op_mul(p, p))
+		if (n & 1u) r = op_mul(p, r);
+	return r;
+}
+Op op_inverse(const Op& m) {  // Gauss-Jordan over GF(2); Z_n is invertible (x is a unit mod P)
+	uint64_t rows[32];        // row i: [63:32] = row i of m, [31:0] = row i of the identity
+	for (int i = 0; i < 32; i++) {
+		uint32_t row = 0;
+		for (int j = 0; j < 32; j++) row |= ((m.c[j] >> i) & 1u) << j;
+		rows[i] = ((uint64_t)row << 32) | (1u << i);
+	}
+	for (int col = 0; col < 32; col++) {
+		int piv = col;
+		while (piv < 32 && !((rows[piv] >> (32 + col)) & 1u)) piv++;
+		if (piv == 32) return op_identity();  // not reached for Z_n
+		std::swap(rows[col], rows[piv]);
+		for (int i = 0; i < 32; i++)
+			if (i != col && ((rows[i] >> (32 + col)) & 1u)) rows[i] ^= rows[col];
+	}
+	Op r;
+	for (int j = 0; j < 32; j++) {
+		uint32_t cj = 0;
+		for (int i = 0; i < 32; i++) cj |= (uint32_t)((rows[i] >> j) & 1u) << i;
+		r.c[j] = cj;
+	}
+	return r;
+}
+
+void be32(uint8_t* p, uint32_t v) {
+	p[0] = (uint8_t)(v >> 24), p[1] = (uint8_t)(v >> 16), p[2] = (uint8_t)(v >> 8), p[3] = (uint8_t)v;
+}
+uint32_t crc32_host(const uint8_t* p, size_t n) {
+	uint32_t c = 0xFFFFFFFFu;
+	for (size_t i = 0; i < n; i++) {
+		c ^= p[i];
+		for (int k = 0; k < 8; k++) c = (c & 1u) ? (c >> 1) ^ 0xEDB88320u : c >> 1;
+	}
+	return ~c;
+}
+
+struct PngOps {
+	uint32_t ops[10][32];
+	uint32_t init;
+};
+// operators depend only on (number of spans, zlib end); cached (frames of one size share them)
+std::mutex g_ops_mu;
+std::map<std::pair<uint32_t, uint32_t>, PngOps> g_ops;
+
+PngOps png_ops(uint32_t G, uint32_t zend) {
+	std::lock_guard<std::mutex> lk(g_ops_mu);
+	auto it = g_ops.find({G, zend});
+	if (it != g_ops.end()) return it->second;
+	PngOps o;
+	const uint32_t m = (G + kThreads - 1u) / kThreads;
+	Op zs = op_zeros(kSpan);
+	memcpy(o.ops[0], zs.c, 128);
+	Op zl = op_zeros((uint64_t)kSpan * m);
+	for (int l = 0; l < kTreeLevels; l++) {
+		memcpy(o.ops[1 + l], zl.c, 128);
+		zl = op_mul(zl, zl);
+	}
+	Op unpad = op_inverse(op_zeros((uint64_t)G * kSpan - zend));
+	memcpy(o.ops[9], unpad.c, 128);
+	o.init = op_host_apply(op_zeros(zend - kCrcStart), 0xFFFFFFFFu);
+	if (g_ops.size() > 256) g_ops.clear();
+	g_ops[{G, zend}] = o;
+	return o;
+}
+
+// the 8 KB constant tables, per device, built once
+std::mutex g_tab_mu;
+uint32_t* g_tab_dev[64];
+
+hipError_t tables_dev(uint32_t** out) {
+	int dev = 0;
+	hipError_t e = hipGetDevice(&dev);
+	if (e != hipSuccess) return e;
+	if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+	std::lock_guard<std::mutex> lk(g_tab_mu);
+	if (!g_tab_dev[dev]) {
+		std::vector<uint32_t> t(kTabWords);
+		for (uint32_t b = 0; b < 256; b++) {
+			uint32_t c = b;
+			for (int k = 0; k < 8; k++) c = (c & 1u) ? (c >> 1) ^ 0xEDB88320u : c >> 1;
+			t[b] = c;
+		}
+		for (int s = 1; s < 4; s++)
+			for (uint32_t b = 0; b < 256; b++) t[256 * s + b] = (t[256 * (s - 1) + b] >> 8) ^ t[t[256 * (s - 1) + b] & 255u];
+		Op z = op_zeros(kPerThread);
+		for (int l = 0; l < kTreeLevels; l++, z = op_mul(z, z))
+			for (int j = 0; j < 8; j++)
+				for (uint32_t v = 0; v < 16; v++) t[1024 + l * 128 + j * 16 + v] = op_host_apply(z, v << (4 * j));
+		uint32_t* p = nullptr;
+		e = hipMalloc((void**)&p, kTabWords * 4);
+		if (e != hipSuccess) return e;
+		e = hipMemcpy(p, t.data(), kTabWords * 4, hipMemcpyHostToDevice);
+		if (e != hipSuccess) {
+			(void)hipFree(p);
+			return e;
+		}
+		g_tab_dev[dev] = p;
+	}
+	*out = g_tab_dev[dev];
+	return hipSuccess;
+}
+
+uint64_t file_size(uint32_t format, uint32_t w, uint32_t h, uint32_t* prefix_len, uint32_t* row_bytes, uint64_t* raw) {
+	if (w == 0 || h == 0 || w > 65535 || h > 65535) return 0;
+	char hdr[64];
+	switch (format) {
+		case VP8G_ENC_RGB:
+			*prefix_len = 0, *row_bytes = 3u * w, *raw = (uint64_t)h * 3u * w;
+			return *raw;
+		case VP8G_ENC_PPM:
+			*prefix_len = (uint32_t)snprintf(hdr, sizeof(hdr), "P6\n%u %u\n255\n", w, h);
+			*row_bytes = 3u * w, *raw = (uint64_t)h * 3u * w;
+			return *prefix_len + *raw;
+		case VP8G_ENC_PNG: {
+			*prefix_len = kPngPrefix, *row_bytes = 1u + 3u * w, *raw = (uint64_t)h * (1u + 3u * w);
+			const uint64_t blocks = (*raw + kBlk - 1u) / kBlk;
+			return kPngPrefix + *raw + 5u * blocks + 4u + 4u + 12u;
+		}
+		default: return 0;
+	}
+}
+
+
+}  // namespace
+
+VP8G_API uint64_t vp8g_encoded_size(uint32_t format, uint32_t width, uint32_t height) {
+	uint32_t pl, rb;
+	uint64_t raw;
+	return file_size(format, width, height, &pl, &rb, &raw);
+}
+
+VP8G_API uint64_t vp8g_encode_workspace_size(uint32_t total_spans) { return 16ull * (total_spans ? total_spans : 1u); }
+
+VP8G_API uint32_t vp8g_make_enc_desc(uint32_t width, uint32_t height, uint32_t format, uint64_t src_y, uint64_t src_u,
+                                     uint64_t src_v, uint32_t stride_y, uint32_t stride_uv, uint64_t out_offset,
+                                     uint32_t span0, Vp8gEncDesc* d) {
+	uint32_t pl = 0, rb = 0;
+	uint64_t raw = 0;
+	const uint64_t flen = d ? file_size(format, width, height, &pl, &rb, &raw) : 0;
+	if (!flen || (out_offset & 15u) || stride_y < width || stride_uv < (width + 1u) / 2u) {
+		errno = EINVAL;
+		return 0;
+	}
+	if (raw > 0x7FFFFFFFu || flen > 0xFFFFFFFFull - 2 * kSpan) {  // the reference's EFBIG bound (yuv2rgb_png.c:241)
+		errno = EFBIG;
+		return 0;
+	}
+	memset(d, 0, sizeof(*d));
+	d->width = width, d->height = height, d->stride_y = stride_y, d->stride_uv = stride_uv;
+	d->src_y = src_y, d->src_u = src_u, d->src_v = src_v;
+	d->out = out_offset, d->file_len = flen;
+	d->format = format, d->prefix_len = pl, d->row_bytes = rb, d->raw_len = (uint32_t)raw;
+	d->span0 = span0;
+	d->nspans = (uint32_t)((flen + kSpan - 1u) / kSpan);
+	if (format == VP8G_ENC_PPM) {
+		snprintf((char*)d->prefix, sizeof(d->prefix), "P6\n%u %u\n255\n", width, height);
+	} else if (format == VP8G_ENC_PNG) {
+		static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', 0x0D, 0x0A, 0x1A, 0x0A};
+		uint8_t* o = d->prefix;
+		memcpy(o, sig, 8);
+		be32(o + 8, 13), memcpy(o + 12, "IHDR", 4);
+		be32(o + 16, width), be32(o + 20, height);
+		o[24] = 8, o[25] = 2, o[26] = 0, o[27] = 0, o[28] = 0;  // 8-bit truecolour, no interlace
+		be32(o + 29, crc32_host(o + 12, 17));
+		const uint64_t zlen = flen - 57u;  // zlib stream: header 2 + blocks + Adler 4 (file: + 41 before, + 16 after)
+		be32(o + 33, (uint32_t)zlen), memcpy(o + 37, "IDAT", 4);
+		o[41] = 0x78, o[42] = 0x01;
+		d->zend = (uint32_t)(flen - 16u);
+		const PngOps ops = png_ops(d->nspans, d->zend);
+		memcpy(d->crc_ops, ops.ops, sizeof(ops.ops));
+		d->crc_init = ops.init;
+	}
+	return d->nspans;
+}
+
+VP8G_API int vp8g_encode_batch_device(const Vp8gEncDesc* h, const Vp8gEncDesc* d_descs, uint32_t n, const uint8_t* d_src,
+                                      uint8_t* d_out, uint8_t* d_work, void* stream) {
+	if (!h || !d_descs || !d_src || !d_out || !d_work || n == 0) {
+		errno = EINVAL;
+		return -1;
+	}
+	uint32_t total = 0;
+	bool any_png = false;
+	for (uint32_t i = 0; i < n; i++) {
+		if (h[i].span0 != total || h[i].nspans == 0) {  // tasks must be numbered image by image
+			errno = EINVAL;
+			return -1;
+		}
+		total += h[i].nspans;
+		any_png |= h[i].format == VP8G_ENC_PNG;
+	}
+	uint32_t* tab = nullptr;
+	hipError_t e = tables_dev(&tab);
+	if (e == hipSuccess) {
+		const int cus = vp8g::device_cus();
+		const uint32_t grid = min(total, (uint32_t)(cus > 0 ? cus : 256) * 12u);
+		hipLaunchKernelGGL(enc_kernel, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, d_descs, n, total, d_src, d_out,
+		                   (uint32_t*)d_work, tab);
+		e = hipGetLastError();
+	}
+	if (e == hipSuccess && any_png) {
+		hipLaunchKernelGGL(png_finish_kernel, dim3(n), dim3(kThreads), 0, (hipStream_t)stream, d_descs, (const uint32_t*)d_work,
+		                   d_out, tab);
+		e = hipGetLastError();
+	}
+	if (e != hipSuccess) {
+		vp8g::set_error_text("encode launch", e);
+		errno = EIO;
+		return -1;
+	}
+	return 0;
+}
+
+// ---- the reference's writers: host image -> device -> file bytes -> fd ---------------------
+namespace {
+struct EncDev {
+	std::mutex mu;
+	hipStream_t stream = nullptr;
+	uint8_t* buf = nullptr;  // source planes | descriptor | workspace | output file
+	size_t cap = 0;
+	uint8_t* host = nullptr;  // pinned staging for the file bytes
+	size_t host_cap = 0;
+};
+EncDev g_enc;
+
+int write_all(int fd, const uint8_t* p, size_t n) {
+	while (n) {
+		const ssize_t w = write(fd, p, n);
+		if (w < 0) {
+			if (errno == EINTR) continue;
+			return -1;
+		}
+		p += w;
+		n -= (size_t)w;
+	}
+	return 0;
+}
+
+int write_image(int fd, const Yuv420Image* img, uint32_t format) {
+	if (fd < 0 || !img || !img->y || !img->u || !img->v || img->width == 0 || img->height == 0 ||
+	    img->stride_y < img->width || img->stride_uv < (img->width + 1u) / 2u) {
+		errno = EINVAL;
+		return -1;
+	}
+	const uint32_t w = img->width, h = img->height, cw = (w + 1u) / 2u, ch = (h + 1u) / 2u;
+	const uint64_t ysz = (uint64_t)w * h, csz = (uint64_t)cw * ch;
+	const uint64_t o_desc = (ysz + 2 * csz + 255u) & ~255ull;
+	Vp8gEncDesc desc;
+	const uint32_t spans = vp8g_make_enc_desc(w, h, format, 0, ysz, ysz + csz, w, cw, 0, 0, &desc);
+	if (!spans) return -1;
+	const uint64_t o_work = o_desc + ((sizeof(Vp8gEncDesc) + 255u) & ~255ull);
+	const uint64_t o_out = (o_work + vp8g_encode_workspace_size(spans) + 255u) & ~255ull;
+	const uint64_t flen = desc.file_len, need = o_out + ((flen + 15u) & ~15ull);
+	std::lock_guard<std::mutex> lk(g_enc.mu);
+	auto fail = [&](const char* where, hipError_t e) {
+		vp8g::set_error_text(where, e);
+		errno = EIO;
+		return -1;
+	};
+	hipError_t e = hipSuccess;
+	if (!g_enc.stream && (e = hipStreamCreateWithFlags(&g_enc.stream, hipStreamNonBlocking)) != hipSuccess)
+		return fail("stream", e);
+	if (need > g_enc.cap) {
+		if (g_enc.buf) (void)hipFree(g_enc.buf);
+		g_enc.buf = nullptr, g_enc.cap = 0;
+		if ((e = hipMalloc((void**)&g_enc.buf, need + need / 4)) != hipSuccess) return fail("hipMalloc", e);
+		g_enc.cap = need + need / 4;
+	}
+	if (flen > g_enc.host_cap) {
+		if (g_enc.host) (void)hipHostFree(g_enc.host);
+		g_enc.host = nullptr, g_enc.host_cap = 0;
+		if ((e = hipHostMalloc((void**)&g_enc.host, flen, hipHostMallocDefault)) != hipSuccess) return fail("hipHostMalloc", e);
+		g_enc.host_cap = flen;
+	}
+	hipStream_t s = g_enc.stream;
+	uint8_t* b = g_enc.buf;
+	desc.out = o_out;  // (the source offsets are relative to b, and so is the output)
+	if ((e = hipMemcpy2DAsync(b, w, img->y, img->stride_y, w, h, hipMemcpyHostToDevice, s)) != hipSuccess ||
+	    (e = hipMemcpy2DAsync(b + ysz, cw, img->u, img->stride_uv, cw, ch, hipMemcpyHostToDevice, s)) != hipSuccess ||
+	    (e = hipMemcpy2DAsync(b + ysz + csz, cw, img->v, img->stride_uv, cw, ch, hipMemcpyHostToDevice, s)) != hipSuccess ||
+	    (e = hipMemcpyAsync(b + o_desc, &desc, sizeof(desc), hipMemcpyHostToDevice, s)) != hipSuccess)
+		return fail("H2D", e);
+	if (vp8g_encode_batch_device(&desc, (const Vp8gEncDesc*)(b + o_desc), 1, b, b, b + o_work, s) != 0) return -1;
+	if ((e = hipMemcpyAsync(g_enc.host, b + o_out, flen, hipMemcpyDeviceToHost, s)) != hipSuccess) return fail("D2H", e);
+	if ((e = hipStreamSynchronize(s)) != hipSuccess) return fail("sync", e);
+	return write_all(fd, g_enc.host, flen);
+}
+}  // namespace
+
+VP8G_API int yuv420_write_ppm_fd(int fd, const Yuv420Image* img) { return write_image(fd, img, VP8G_ENC_PPM); }
+
+VP8G_API int yuv420_write_png_fd(int fd, const Yuv420Image* img) { return write_image(fd, img, VP8G_ENC_PNG); }

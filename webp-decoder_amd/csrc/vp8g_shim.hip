@@ -499,4 +499,6 @@ VP8G_API int vp8_loopfilter_apply_keyframe(Yuv420Image* img, const Vp8DecodedFra
 
 VP8G_API const char* vp8g_last_error(void) { return g_err; }
 
+void vp8g::set_error_text(const char* where, hipError_t e) { set_err(where, e); }
+
 VP8G_API uint32_t vp8g_abi_version(void) { return VP8G_ABI_VERSION; }

@@ -5,9 +5,12 @@
  *   decoder -info <file.webp>
  *   decoder -yuv  <file.webp> <out.i420>    recon only            (m06 on the GPU)
  *   decoder -yuvf <file.webp> <out.i420>    recon + loop filter   (m06 + m07 on the GPU)
+ *   decoder -ppm  <file.webp> <out.ppm>     recon + loop filter + RGB (m08 writer, on the GPU)
+ *   decoder -png  <file.webp> <out.png>     recon + loop filter + RGB (m09 writer, on the GPU)
  *   decoder -diff_mb <file.webp> <oracle.i420>   per-macroblock SAD of our -yuv vs a file
  *
- * Output: raw I420, Y (w*h) then U then V (each ceil(w/2)*ceil(h/2)), no header.
+ * Output (-yuv/-yuvf): raw I420, Y (w*h) then U then V (each ceil(w/2)*ceil(h/2)), no header;
+ * -ppm / -png: the files of yuv420_write_ppm_fd / yuv420_write_png_fd (reference src/main.c:706-844).
  * Exit codes: 0 ok, 1 failure (message on stderr), 2 usage.
  * The host front end (container, header, token decode) runs on the CPU; reconstruction goes
  * through libvp8g.so's reference entry points (vp8_reconstruct_keyframe_yuv[_filtered]).
@@ -27,6 +30,8 @@ static void usage(void) {
 	fputs("  decoder -info <file.webp>\n", stderr);
 	fputs("  decoder -yuv <file.webp> <out.i420>\n", stderr);
 	fputs("  decoder -yuvf <file.webp> <out.i420>\n", stderr);
+	fputs("  decoder -ppm <file.webp> <out.ppm>\n", stderr);
+	fputs("  decoder -png <file.webp> <out.png>\n", stderr);
 	fputs("  decoder -diff_mb <file.webp> <oracle.i420>\n", stderr);
 }
 
@@ -81,6 +86,37 @@ static int cmd_yuv(const char* in, const char* out_path, int filtered) {
 	yuv420_free(&img);
 	if (w != 0) {
 		fputs("error: write failed\n", stderr);
+		return 1;
+	}
+	return 0;
+}
+
+/* reference src/main.c:706-773 (-ppm) and :775-844 (-png): filtered reconstruction, then the
+ * m08 / m09 writer into the output file */
+static int cmd_rgb(const char* in, const char* out_path, int png) {
+	Vp8KeyFrameHeader kf;
+	Vp8DecodedFrame d;
+	if (front(in, &kf, &d) != 0) return 1;
+	Yuv420Image img;
+	int rc = vp8_reconstruct_keyframe_yuv_filtered(&kf, &d, &img);
+	vp8_decoded_frame_free(&d);
+	if (rc != 0) {
+		fputs("error: VP8 reconstruction/loopfilter failed\n", stderr);
+		const char* he = vp8g_last_error();
+		if (he && *he) fprintf(stderr, "  (%s)\n", he);
+		return 1;
+	}
+	int fd = open(out_path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+	if (fd < 0) {
+		fputs("error: cannot open output file\n", stderr);
+		yuv420_free(&img);
+		return 1;
+	}
+	int wrc = png ? yuv420_write_png_fd(fd, &img) : yuv420_write_ppm_fd(fd, &img);
+	close(fd);
+	yuv420_free(&img);
+	if (wrc != 0) {
+		fputs(png ? "error: PNG write failed\n" : "error: PPM write failed\n", stderr);
 		return 1;
 	}
 	return 0;
@@ -175,6 +211,13 @@ int main(int argc, char** argv) {
 			return 2;
 		}
 		return cmd_yuv(argv[2], argv[3], cmd[4] == 'f');
+	}
+	if (!strcmp(cmd, "-ppm") || !strcmp(cmd, "-png")) {
+		if (argc != 4) {
+			usage();
+			return 2;
+		}
+		return cmd_rgb(argv[2], argv[3], cmd[2] == 'n');
 	}
 	if (!strcmp(cmd, "-diff_mb")) {
 		if (argc != 4) {

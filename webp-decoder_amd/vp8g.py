@@ -100,6 +100,21 @@ class Vp8gBatchArrays(C.Structure):
         "bmode", "src", "status")]
 
 
+class Vp8gEncDesc(C.Structure):
+    _fields_ = [
+        ("width", C.c_uint32), ("height", C.c_uint32), ("stride_y", C.c_uint32), ("stride_uv", C.c_uint32),
+        ("src_y", C.c_uint64), ("src_u", C.c_uint64), ("src_v", C.c_uint64), ("out", C.c_uint64),
+        ("file_len", C.c_uint64), ("format", C.c_uint32), ("prefix_len", C.c_uint32), ("row_bytes", C.c_uint32),
+        ("raw_len", C.c_uint32), ("span0", C.c_uint32), ("nspans", C.c_uint32), ("zend", C.c_uint32),
+        ("crc_init", C.c_uint32), ("prefix", C.c_uint8 * 48), ("reserved", C.c_uint32 * 4),
+        ("crc_ops", (C.c_uint32 * 32) * 10),
+    ]
+
+
+ENC_FORMATS = {"rgb": 0, "ppm": 1, "png": 2}
+ENC_SPAN = 32768
+
+assert C.sizeof(Vp8gEncDesc) == 1432
 assert C.sizeof(Vp8KeyFrameHeader) == 28
 assert C.sizeof(Vp8CoeffStats) == 200
 assert C.sizeof(Vp8DecodedFrame) == 320
@@ -175,6 +190,17 @@ def gpu_lib():
         lib.vp8g_reconstruct_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int, P(Yuv420Image)]
         lib.vp8g_last_error.restype = C.c_char_p
         lib.vp8g_abi_version.restype = C.c_uint32
+        lib.yuv420_write_ppm_fd.argtypes = [C.c_int, P(Yuv420Image)]
+        lib.yuv420_write_png_fd.argtypes = [C.c_int, P(Yuv420Image)]
+        lib.vp8g_encoded_size.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32]
+        lib.vp8g_encoded_size.restype = C.c_uint64
+        lib.vp8g_encode_workspace_size.argtypes = [C.c_uint32]
+        lib.vp8g_encode_workspace_size.restype = C.c_uint64
+        lib.vp8g_make_enc_desc.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64,
+                                           C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32, P(Vp8gEncDesc)]
+        lib.vp8g_make_enc_desc.restype = C.c_uint32
+        lib.vp8g_encode_batch_device.argtypes = [P(Vp8gEncDesc), C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
+                                                 C.c_void_p, C.c_void_p]
         lib._typed = True
     return lib
 
@@ -273,6 +299,41 @@ def gpu_reconstruct_batch(frames: list[Frame], filtered: bool) -> list[bytes]:
         out.append(_image_bytes(imgs[i]))
         lib.yuv420_free(C.byref(imgs[i]))
     return out
+
+
+def gpu_encode(i420: bytes, w: int, h: int, fmt: str) -> bytes:
+    """The reference's m08/m09 writers (yuv420_write_ppm_fd / yuv420_write_png_fd) through
+    libvp8g.so: the file they write for a cropped I420 image."""
+    import tempfile
+    lib = gpu_lib()
+    img, keep = image_from_i420(i420, w, h)
+    fn = lib.yuv420_write_ppm_fd if fmt == "ppm" else lib.yuv420_write_png_fd
+    with tempfile.TemporaryFile() as t:
+        if fn(t.fileno(), C.byref(img)) != 0:
+            raise RuntimeError(f"vp8g {fmt} writer failed: errno={C.get_errno()} {lib.vp8g_last_error()!r}")
+        t.seek(0)
+        data = t.read()
+    del keep
+    return data
+
+
+def make_enc_descs(sizes, fmt: str, src_offsets, out_align: int = 256):
+    """Descriptors for images of the given (w, h) sizes whose planes sit at src_offsets[i] =
+    (y, u, v) with tight strides, outputs packed at out_align-aligned offsets.  Returns
+    (array of Vp8gEncDesc, output offsets, total output bytes, total tasks)."""
+    lib = gpu_lib()
+    n = len(sizes)
+    descs = (Vp8gEncDesc * n)()
+    outs, o, span0 = [], 0, 0
+    for i, (w, h) in enumerate(sizes):
+        y, u, v = src_offsets[i]
+        k = lib.vp8g_make_enc_desc(w, h, ENC_FORMATS[fmt], y, u, v, w, (w + 1) // 2, o, span0, C.byref(descs[i]))
+        if k == 0:
+            raise ValueError(f"vp8g_make_enc_desc failed for {w}x{h} {fmt}")
+        outs.append(o)
+        o = (o + descs[i].file_len + out_align - 1) // out_align * out_align
+        span0 += k
+    return descs, outs, o, span0
 
 
 def make_desc(f: Frame, filtered: bool, mb_offset: int, out_offset: int) -> Vp8gFrameDesc:
