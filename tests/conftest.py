@@ -10,6 +10,11 @@ import sys
 
 import pytest
 
+# torch bundles its own HIP runtime under the same soname as /opt/rocm's: whichever loads first
+# serves the whole process.  Load torch's first (as bench.py does), so that tests which allocate
+# device memory with torch after libvp8g.so has run still see the GPU.
+import torch  # noqa: F401,E402
+
 ROOT = pathlib.Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT / "webp-decoder_amd"))
 
