@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
+    ap.add_argument("--encode", default="png", choices=["none", "rgb", "ppm", "png"],
+                    help="also time the m08/m09 stage on the batch's output (secondary object 'encode')")
     return ap.parse_args()
 
 
@@ -115,6 +117,36 @@ class Batch:
     def frame_output(self, i: int, w: int, h: int) -> bytes:
         o = i * self.frame_bytes
         return self.out[o:o + vp8g.i420_size(w, h)].cpu().numpy().tobytes()
+
+
+class EncodeStage:
+    """m08/m09 on the device: the batch's I420 outputs -> RGB / PPM / PNG files.
+    Algorithmic bytes per frame: the I420 read once (w*h*1.5) + the file written."""
+
+    def __init__(self, batch: "Batch", W: int, H: int, fmt: str, dev):
+        cw, ch = (W + 1) // 2, (H + 1) // 2
+        offs = [(i * batch.frame_bytes, i * batch.frame_bytes + W * H, i * batch.frame_bytes + W * H + cw * ch)
+                for i in range(batch.n)]
+        self.fmt = fmt
+        self.descs, self.outs, total, spans = vp8g.make_enc_descs([(W, H)] * batch.n, fmt, offs)
+        self.d_descs = torch.frombuffer(bytearray(bytes(self.descs)), dtype=torch.uint8).to(dev)
+        self.out = torch.empty(total, dtype=torch.uint8, device=dev)
+        self.work = torch.empty(vp8g.gpu_lib().vp8g_encode_workspace_size(spans), dtype=torch.uint8, device=dev)
+        self.src = batch.out
+        self.n = batch.n
+        self.file_len = self.descs[0].file_len
+        self.bytes = batch.n * (vp8g.i420_size(W, H) + self.file_len)
+
+    def launch(self, stream):
+        rc = vp8g.gpu_lib().vp8g_encode_batch_device(self.descs, C.c_void_p(self.d_descs.data_ptr()), self.n,
+                                                      C.c_void_p(self.src.data_ptr()), C.c_void_p(self.out.data_ptr()),
+                                                      C.c_void_p(self.work.data_ptr()), C.c_void_p(stream))
+        if rc != 0:
+            raise RuntimeError(f"encode launch failed: {vp8g.gpu_lib().vp8g_last_error()!r}")
+
+    def file(self, i: int) -> bytes:
+        o = self.outs[i]
+        return self.out[o:o + self.file_len].cpu().numpy().tobytes()
 
 
 def cpu_baseline(frames, filtered, threads, seconds):
@@ -206,6 +238,35 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(frames, filtered, args.cpu_threads, args.cpu_seconds)
 
+    enc_obj = None
+    if args.encode != "none" and filtered:
+        enc = EncodeStage(batch, W, H, args.encode, dev)
+        for _ in range(max(1, args.warmup)):
+            enc.launch(stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        eevs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+        for s in range(args.steps):
+            eevs[s][0].record(stream)
+            enc.launch(stream.cuda_stream)
+            eevs[s][1].record(stream)
+        torch.cuda.synchronize(dev)
+        enc_ms = sum(a.elapsed_time(b) for a, b in eevs) / args.steps
+        fkey = {"ppm": "ppm_sha256", "png": "png_sha256"}.get(args.encode)
+        if fkey:
+            enc_ok = all(hashlib.sha256(enc.file(i)).hexdigest() == manifest["files"][FIXTURES[i % 4]][fkey]
+                         for i in range(min(4, args.frames)))
+        else:
+            enc_ok = None
+        enc_gbs = enc.bytes / (enc_ms * 1e-3) / 1e9
+        enc_obj = {"stage": f"m08/m09 I420 -> {args.encode.upper()} files on the device (one launch over the batch"
+                            + (" + checksum finish" if args.encode == "png" else "") + ")",
+                   "kernel_ms_per_step": round(enc_ms, 3),
+                   "value": round(args.frames * W * H / 1e6 / (enc_ms * 1e-3), 1), "unit": "MP/s",
+                   "parity": None if enc_ok is None else ("bit-exact vs reference (4 slots sha256)" if enc_ok else "MISMATCH"),
+                   "roofline": {"bound": "hbm", "achieved": round(enc_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                                "frac": round(enc_gbs / PEAK_HBM_GBS, 4),
+                                "algorithmic_bytes_per_launch": enc.bytes}}
+
     stamp_shares = None
     if stamps:
         acc = (C.c_ulonglong * 16)()
@@ -245,6 +306,8 @@ def main():
                          "binding_resource": "vector-instruction issue (VALU), see DESIGN.md §5"},
             "cpu_baseline": cpu,
         }
+        if enc_obj:
+            line["encode"] = enc_obj
         if stamp_shares:
             line["stamps"] = stamp_shares
         print(json.dumps(line), flush=True)

@@ -7,9 +7,9 @@
 //      pair shares its four chroma samples and the 9:3:3:1 diagonals) and the few layout bytes
 //      (PPM header; PNG signature / IHDR / IDAT header / zlib header, the 5-byte stored-block
 //      headers, the IEND trailer) into an LDS image of the span;
-//   2. streams the span to HBM as 16-byte stores, 128 contiguous bytes per thread, and -- PNG --
-//      folds the same bytes into a CRC-32 (slice-by-4 tables) and Adler-32 partial sums;
-//   3. combines the 256 thread CRCs with GF(2) shift operators (nibble tables in LDS) into one
+//   2. streams the span to HBM as 16-byte stores, 64 contiguous bytes per thread, and -- PNG --
+//      folds the same bytes into a CRC-32 (slice-by-8 tables) and Adler-32 partial sums;
+//   3. combines the 512 thread CRCs with GF(2) shift operators (nibble tables in LDS) into one
 //      CRC per span, written with the span's Adler partials to the workspace.
 // A second, small launch (one workgroup per PNG) combines the span partials and writes the
 // Adler-32 and the IDAT CRC.  Every byte of every file is produced on the device.
@@ -39,20 +39,25 @@
 namespace {
 
 constexpr uint32_t kSpan = VP8G_ENC_SPAN;
-constexpr int kThreads = 256;
-constexpr uint32_t kPerThread = kSpan / kThreads;  // 128 contiguous file bytes per thread
+constexpr int kThreads = 1024;                     // task kernel
+constexpr uint32_t kPerThread = kSpan / kThreads;  // 32 contiguous file bytes per thread
+constexpr int kFinThreads = 256;                   // PNG finishing kernel
+constexpr int kFinLevels = 8;                      // log2(kFinThreads)
+constexpr uint32_t kGroup = 4;                     // pixel-pair units per thread and iteration
 constexpr uint32_t kMod = 65521u;                  // Adler-32
 constexpr uint32_t kBlk = 65535u;                  // stored-deflate block payload
 constexpr uint32_t kBlkFile = kBlk + 5u;           // ... plus its header
 constexpr uint32_t kPngPrefix = 43u;               // signature 8, IHDR 25, IDAT len/type 8, zlib 2
 constexpr uint32_t kPngRaw0 = kPngPrefix + 5u;     // file offset of the first pixel-stream byte
 constexpr uint32_t kCrcStart = 37u;                // IDAT CRC covers the chunk type + data
-constexpr int kTreeLevels = 8;                     // log2(kThreads)
+constexpr int kTreeLevels = 10;                    // log2(kThreads)
 static_assert(kSpan % kThreads == 0 && kPerThread % 16 == 0, "span layout");
 
-// Tables shared by every task (8 KB): CRC-32 slice-by-4 tables T0..T3, then for the in-span tree
-// the nibble tables of Z_{128 * 2^l}, l = 0..7: tab[l][j][v] = Z(v << 4j).
-constexpr int kTabWords = 4 * 256 + kTreeLevels * 8 * 16;
+// Tables shared by every task (12.5 KB): CRC-32 slice-by-8 tables T0..T7, then for the in-span
+// tree the nibble tables of Z_{64 * 2^l}, l = 0..8: tab[2048 + 128 l + 16 j + v] = Z(v << 4j).
+constexpr int kSlice = 8;
+constexpr int kNibBase = kSlice * 256;
+constexpr int kTabWords = kNibBase + kTreeLevels * 8 * 16;
 
 struct EncLds {
 	uint8_t buf[kSpan];
@@ -62,7 +67,10 @@ struct EncLds {
 
 // ---- device helpers ----------------------------------------------------------------------
 // reference yuv2rgb_ppm.c:19-42: libwebp VP8YuvToRgb (14-bit fixed point, clip of v >> 6)
-DEV uint32_t clip6(int v) { return (uint32_t)min(max(v >> 6, 0), 255); }
+// Clamp before the shift (same result as clip(v >> 6)): the shift-then-clamp form of two
+// neighbouring channels is selected as v_ashr_pk_u8_i32, whose result here kept the old upper 16
+// bits of its destination register, which then leaked into the packed colour word.
+DEV uint32_t clip6(int v) { return (uint32_t)min(max(v, 0), 16383) >> 6; }
 DEV uint32_t yuv_rgb(int y, int u, int v) {  // packed r | g << 8 | b << 16
 	const int yy = (y * 19077) >> 8;
 	const uint32_t r = clip6(yy + ((v * 26149) >> 8) - 14234);
@@ -82,9 +90,10 @@ DEV uint32_t raw_of_file(const Vp8gEncDesc& d, uint32_t q) {
 }
 
 DEV uint32_t crc_byte(const uint32_t* t0, uint32_t c, uint32_t b) { return t0[(c ^ b) & 255u] ^ (c >> 8); }
-DEV uint32_t crc_word(const uint32_t* t, uint32_t c, uint32_t w) {  // slice-by-4 (little-endian word)
-	c ^= w;
-	return t[768 + (c & 255u)] ^ t[512 + ((c >> 8) & 255u)] ^ t[256 + ((c >> 16) & 255u)] ^ t[c >> 24];
+DEV uint32_t crc_dword2(const uint32_t* t, uint32_t c, uint32_t w0, uint32_t w1) {  // slice-by-8, 8 bytes
+	c ^= w0;
+	return t[1792 + (c & 255u)] ^ t[1536 + ((c >> 8) & 255u)] ^ t[1280 + ((c >> 16) & 255u)] ^ t[1024 + (c >> 24)] ^
+	       t[768 + (w1 & 255u)] ^ t[512 + ((w1 >> 8) & 255u)] ^ t[256 + ((w1 >> 16) & 255u)] ^ t[w1 >> 24];
 }
 DEV uint32_t nib_apply(const uint32_t* nt, uint32_t v) {  // GF(2) operator via 8 nibble tables
 	uint32_t r = 0;
@@ -100,7 +109,7 @@ DEV uint32_t op_apply(const uint32_t* col, uint32_t v) {  // GF(2) operator by c
 }
 
 // ---- task kernel -------------------------------------------------------------------------
-__global__ __launch_bounds__(kThreads) void enc_kernel(const Vp8gEncDesc* __restrict__ D, uint32_t n, uint32_t total,
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void enc_kernel(const Vp8gEncDesc* __restrict__ D, uint32_t n, uint32_t total,
                                                        const uint8_t* __restrict__ src, uint8_t* __restrict__ out,
                                                        uint32_t* __restrict__ part, const uint32_t* __restrict__ tables) {
 	__shared__ EncLds L;
@@ -127,51 +136,87 @@ __global__ __launch_bounds__(kThreads) void enc_kernel(const Vp8gEncDesc* __rest
 			const uint8_t* Y = src + d.src_y;
 			const uint8_t* U = src + d.src_u;
 			const uint8_t* V = src + d.src_v;
-			for (uint32_t gu = gu0 + tid; gu < gu1; gu += kThreads) {
-				// (row, unit) = divmod(gu, UPR): float estimate, exact after the corrections
-				int y = (int)((float)gu * inv);
-				int k = (int)gu - y * (int)UPR;
-				while (k < 0) k += (int)UPR, y--;
-				while (k >= (int)UPR) k -= (int)UPR, y++;
-				// chroma rows (reference yuv2rgb_ppm.c:178-202): row 0 uses row 0 twice; row y
-				// sits between a = (y-1)/2 and b = min(a+1, ch-1), nearer a when y is odd
-				const uint32_t a = y ? (uint32_t)(y - 1) >> 1 : 0u, b = y ? min(a + 1u, ch - 1u) : 0u;
-				const bool near_a = y == 0 || (y & 1);
-				// columns (reference yuv2rgb_ppm.c:44-121): the pair (2k-1, 2k) blends columns k-1 and
-				// k; at the edges both are the same column, which gives the 3:1 edge formula exactly
-				const uint32_t cl = k ? (uint32_t)k - 1u : 0u, cr = min((uint32_t)k, cw - 1u);
-				const size_t ra = (size_t)a * d.stride_uv, rb = (size_t)b * d.stride_uv;
-				const int tlu = U[ra + cl], tu = U[ra + cr], lu = U[rb + cl], uu = U[rb + cr];
-				const int tlv = V[ra + cl], tv = V[ra + cr], lv = V[rb + cl], uv = V[rb + cr];
+			// One unit = pixels {2k-1, 2k} of row y.  Chroma rows (reference yuv2rgb_ppm.c:178-202):
+			// row 0 uses row 0 twice; row y sits between a = (y-1)/2 and b = min(a+1, ch-1), nearer a
+			// when y is odd.  Columns (yuv2rgb_ppm.c:44-121): the pair blends columns k-1 and k; at the
+			// edges both are one column, which gives the 3:1 edge formula exactly.  Each returns the
+			// two pixels' colours (r | g << 8 | b << 16) from the 2x2 chroma samples (tl, t, l, u).
+			auto pair_rgb = [](bool near_a, int tlu, int tu, int lu, int uu, int tlv, int tv, int lv, int uv, int y_odd,
+			                   int y_even, uint32_t& c_odd, uint32_t& c_even) {
 				const int au = tlu + tu + lu + uu + 8, av = tlv + tv + lv + uv + 8;
 				const int d12u = (au + 2 * (tu + lu)) >> 3, d03u = (au + 2 * (tlu + uu)) >> 3;
 				const int d12v = (av + 2 * (tv + lv)) >> 3, d03v = (av + 2 * (tlv + uv)) >> 3;
-				const int u_odd = near_a ? (d12u + tlu) >> 1 : (d03u + lu) >> 1;
-				const int v_odd = near_a ? (d12v + tlv) >> 1 : (d03v + lv) >> 1;
-				const int u_even = near_a ? (d03u + tu) >> 1 : (d12u + uu) >> 1;
-				const int v_even = near_a ? (d03v + tv) >> 1 : (d12v + uv) >> 1;
-				const uint8_t* yr = Y + (size_t)y * d.stride_y;
-				const bool has_odd = k > 0, has_even = 2u * (uint32_t)k < W;
-				const uint32_t x_odd = 2u * (uint32_t)k - 1u, x_even = 2u * (uint32_t)k;
-				// (indices clamped so that no load is ever out of the plane, even if speculated)
-				const uint32_t c_odd = has_odd ? yuv_rgb(yr[has_odd ? x_odd : 0u], u_odd, v_odd) : 0u;
-				const uint32_t c_even = has_even ? yuv_rgb(yr[has_even ? x_even : x_odd], u_even, v_even) : 0u;
-				// bytes: [filter byte (PNG, k == 0)] [odd pixel] [even pixel], at raw offsets from p0
-				const uint32_t rowp = (uint32_t)y * SB;
-				const uint32_t pb = k ? rowp + f + 3u * x_odd : rowp;  // first byte this unit writes
-				const uint32_t nb = (k ? 0u : f) + (has_odd ? 3u : 0u) + (has_even ? 3u : 0u);
-				uint32_t qb, bnd = 0xFFFFFFFFu;
-				if (png) {
-					const uint32_t blk = pb / kBlk;
-					qb = kPngRaw0 + pb + 5u * blk;
-					bnd = (blk + 1u) * kBlk;  // raw offset where the next block header intervenes
-				} else {
-					qb = d.prefix_len + pb;
+				c_odd = yuv_rgb(y_odd, near_a ? (d12u + tlu) >> 1 : (d03u + lu) >> 1, near_a ? (d12v + tlv) >> 1 : (d03v + lv) >> 1);
+				c_even = yuv_rgb(y_even, near_a ? (d03u + tu) >> 1 : (d12u + uu) >> 1, near_a ? (d03v + tv) >> 1 : (d12v + uv) >> 1);
+			};
+			for (uint32_t g0 = gu0 + kGroup * tid; g0 < gu1; g0 += kGroup * kThreads) {
+				// (row, unit) of the group's first unit = divmod(g0, UPR): float estimate + corrections
+				int y0 = (int)((float)g0 * inv);
+				int k0 = (int)g0 - y0 * (int)UPR;
+				while (k0 < 0) k0 += (int)UPR, y0--;
+				while (k0 >= (int)UPR) k0 -= (int)UPR, y0++;
+				const uint32_t a0 = y0 ? (uint32_t)(y0 - 1) >> 1 : 0u, b0 = y0 ? min(a0 + 1u, ch - 1u) : 0u;
+				const bool near0 = y0 == 0 || (y0 & 1);
+				// fast group: 4 inner units of one row (8 pixels, 24 contiguous bytes of one stored block)
+				// inside the span
+				const uint32_t p0 = (uint32_t)y0 * SB + f + 3u * (2u * (uint32_t)k0 - 1u);
+				const uint32_t q0 = png ? kPngRaw0 + p0 + 5u * (p0 / kBlk) : d.prefix_len + p0;
+				const bool fast = k0 >= 1 && 2u * ((uint32_t)k0 + kGroup - 1u) < W && g0 + kGroup <= gu1 &&
+				                  (!png || p0 / kBlk == (p0 + 3u * 2u * kGroup - 1u) / kBlk) && q0 >= F0 &&
+				                  q0 + 3u * 2u * kGroup <= F0 + kSpan;
+				if (fast) {
+					// chroma columns k0-1 .. k0+3 of rows a, b; luma x = 2k0-1 .. 2k0+6 (32-bit offsets
+					// from the uniform plane bases)
+					const uint32_t ua = a0 * d.stride_uv + (uint32_t)k0 - 1u, ub = b0 * d.stride_uv + (uint32_t)k0 - 1u;
+					const uint32_t yo = (uint32_t)y0 * d.stride_y + 2u * (uint32_t)k0 - 1u;
+					int ca[5], cb[5], va[5], vb[5], yv[8];
+#pragma unroll
+					for (int j = 0; j < 5; j++) ca[j] = U[ua + j], cb[j] = U[ub + j], va[j] = V[ua + j], vb[j] = V[ub + j];
+#pragma unroll
+					for (int j = 0; j < 8; j++) yv[j] = Y[yo + j];
+					uint8_t* o = L.buf + (q0 - F0);
+#pragma unroll
+					for (int i = 0; i < (int)kGroup; i++) {
+						uint32_t c_odd, c_even;
+						pair_rgb(near0, ca[i], ca[i + 1], cb[i], cb[i + 1], va[i], va[i + 1], vb[i], vb[i + 1], yv[2 * i],
+						         yv[2 * i + 1], c_odd, c_even);
+						o[6 * i + 0] = (uint8_t)c_odd, o[6 * i + 1] = (uint8_t)(c_odd >> 8), o[6 * i + 2] = (uint8_t)(c_odd >> 16);
+						o[6 * i + 3] = (uint8_t)c_even, o[6 * i + 4] = (uint8_t)(c_even >> 8), o[6 * i + 5] = (uint8_t)(c_even >> 16);
+					}
+					continue;
 				}
-				uint64_t bytes = k ? ((uint64_t)c_even << 24) | c_odd : (f ? ((uint64_t)c_even << 8) : (uint64_t)c_even);
-				for (uint32_t i = 0; i < nb; i++) {
-					const uint32_t q = qb + i + ((pb + i >= bnd) ? 5u : 0u) - F0;
-					if (q < kSpan) L.buf[q] = (uint8_t)(bytes >> (8 * i));
+				// generic units (row ends, span / block boundaries, narrow images)
+				for (uint32_t j = 0; j < kGroup; j++) {
+					if (g0 + j >= gu1) break;
+					int y = y0, k = k0 + (int)j;
+					while (k >= (int)UPR) k -= (int)UPR, y++;
+					const uint32_t a = y ? (uint32_t)(y - 1) >> 1 : 0u, b = y ? min(a + 1u, ch - 1u) : 0u;
+					const bool near_a = y == 0 || (y & 1);
+					const uint32_t cl = k ? (uint32_t)k - 1u : 0u, cr = min((uint32_t)k, cw - 1u);
+					const uint32_t ra = a * d.stride_uv, rb = b * d.stride_uv, yr = (uint32_t)y * d.stride_y;
+					const bool has_odd = k > 0, has_even = 2u * (uint32_t)k < W;
+					uint32_t c_odd, c_even;
+					// (indices clamped so that no load leaves the plane)
+					pair_rgb(near_a, U[ra + cl], U[ra + cr], U[rb + cl], U[rb + cr], V[ra + cl], V[ra + cr], V[rb + cl],
+					         V[rb + cr], Y[yr + (k ? 2u * (uint32_t)k - 1u : 0u)], Y[yr + min(2u * (uint32_t)k, W - 1u)], c_odd,
+					         c_even);
+					// bytes: [filter byte (PNG, k == 0)] [odd pixel] [even pixel], from raw offset pb
+					const uint32_t rowp = (uint32_t)y * SB;
+					const uint32_t pb = k ? rowp + f + 3u * (2u * (uint32_t)k - 1u) : rowp;
+					const uint32_t nb = (k ? 0u : f) + (has_odd ? 3u : 0u) + (has_even ? 3u : 0u);
+					uint32_t qb, bnd = 0xFFFFFFFFu;
+					if (png) {
+						const uint32_t blk = pb / kBlk;
+						qb = kPngRaw0 + pb + 5u * blk;
+						bnd = (blk + 1u) * kBlk;  // raw offset where the next block header intervenes
+					} else {
+						qb = d.prefix_len + pb;
+					}
+					const uint64_t bytes = k ? ((uint64_t)c_even << 24) | c_odd : (f ? ((uint64_t)c_even << 8) : (uint64_t)c_even);
+					for (uint32_t i = 0; i < nb; i++) {
+						const uint32_t q = qb + i + ((pb + i >= bnd) ? 5u : 0u) - F0;
+						if (q < kSpan) L.buf[q] = (uint8_t)(bytes >> (8 * i));
+					}
 				}
 			}
 		}
@@ -201,7 +246,7 @@ __global__ __launch_bounds__(kThreads) void enc_kernel(const Vp8gEncDesc* __rest
 		}
 		__syncthreads();
 
-		// -- 2. stream 128 contiguous bytes per thread to HBM (+ PNG checksum partials)
+		// -- 2. stream 64 contiguous bytes per thread to HBM (+ PNG checksum partials)
 		const uint32_t q0 = F0 + tid * kPerThread;
 		const uint32_t* bw = (const uint32_t*)(L.buf + tid * kPerThread);
 		uint8_t* dst = out + d.out + q0;
@@ -215,14 +260,15 @@ __global__ __launch_bounds__(kThreads) void enc_kernel(const Vp8gEncDesc* __rest
 			const uint32_t p0 = k0 * kBlk + o0 - 5u;
 			const bool fast = q0 >= kPngRaw0 && o0 >= 5u && o0 + kPerThread <= kBlkFile && p0 + kPerThread <= N;
 			if (fast) {
-				// all 128 bytes are pixel-stream bytes of one stored block (inside the CRC range)
+				// all 64 bytes are pixel-stream bytes of one stored block (inside the CRC range)
 				uint32_t sj = 0;
-#pragma unroll 8
-				for (uint32_t i = 0; i < kPerThread / 4u; i++) {
-					const uint32_t w = bw[i];
-					c = crc_word(L.tab, c, w);
-					s0 = __builtin_amdgcn_sad_u8(w, 0u, s0);
-					sj = __builtin_amdgcn_udot4(w, 0x03020100u + 0x04040404u * i, sj, false);
+#pragma unroll
+				for (uint32_t i = 0; i < kPerThread / 4u; i += 2) {
+					const uint32_t w0 = bw[i], w1 = bw[i + 1];
+					c = crc_dword2(L.tab, c, w0, w1);
+					s0 = __builtin_amdgcn_sad_u8(w1, 0u, __builtin_amdgcn_sad_u8(w0, 0u, s0));
+					sj = __builtin_amdgcn_udot4(w0, 0x03020100u + 0x04040404u * i, sj, false);
+					sj = __builtin_amdgcn_udot4(w1, 0x03020100u + 0x04040404u * (i + 1), sj, false);
 				}
 				// Adler b-sum: sum over bytes of (N - p) r_p = (N - p0) s0 - sum j r_j (mod 65521)
 				const uint32_t w0 = (N - p0) % kMod;
@@ -244,10 +290,10 @@ __global__ __launch_bounds__(kThreads) void enc_kernel(const Vp8gEncDesc* __rest
 				}
 			} else {
 				// past the CRC range: zero bytes (the padded tail of the last span)
-#pragma unroll 8
-				for (uint32_t i = 0; i < kPerThread / 4u; i++) c = crc_word(L.tab, c, 0u);
+#pragma unroll
+				for (uint32_t i = 0; i < kPerThread / 4u; i += 2) c = crc_dword2(L.tab, c, 0u, 0u);
 			}
-			// -- 3. span CRC: tree over the 256 thread CRCs (each over 128 bytes)
+			// -- 3. span CRC: tree over the 512 thread CRCs (each over 64 bytes)
 			L.red[0][tid] = c;
 			L.red[1][tid] = s0;
 			L.red[2][tid] = s1;
@@ -255,7 +301,7 @@ __global__ __launch_bounds__(kThreads) void enc_kernel(const Vp8gEncDesc* __rest
 				__syncthreads();
 				if (tid < (uint32_t)(kThreads >> (l + 1))) {
 					const uint32_t lo = tid << (l + 1), hi = lo + (1u << l);
-					L.red[0][lo] = nib_apply(L.tab + 1024 + l * 128, L.red[0][lo]) ^ L.red[0][hi];
+					L.red[0][lo] = nib_apply(L.tab + kNibBase + l * 128, L.red[0][lo]) ^ L.red[0][hi];
 					L.red[1][lo] = (L.red[1][lo] + L.red[1][hi]) % kMod;
 					L.red[2][lo] = (L.red[2][lo] + L.red[2][hi]) % kMod;
 				}
@@ -271,13 +317,13 @@ __global__ __launch_bounds__(kThreads) void enc_kernel(const Vp8gEncDesc* __rest
 }
 
 // ---- PNG finishing kernel: one workgroup per image ---------------------------------------
-__global__ __launch_bounds__(kThreads) void png_finish_kernel(const Vp8gEncDesc* __restrict__ D,
+__global__ __launch_bounds__(kFinThreads) void png_finish_kernel(const Vp8gEncDesc* __restrict__ D,
                                                               const uint32_t* __restrict__ part, uint8_t* __restrict__ out,
                                                               const uint32_t* __restrict__ tables) {
-	__shared__ uint32_t red[3][kThreads];
+	__shared__ uint32_t red[3][kFinThreads];
 	const Vp8gEncDesc& d = D[blockIdx.x];
 	if (d.format != VP8G_ENC_PNG) return;
-	const uint32_t tid = threadIdx.x, G = d.nspans, m = (G + kThreads - 1u) / kThreads, pad = m * kThreads - G;
+	const uint32_t tid = threadIdx.x, G = d.nspans, m = (G + kFinThreads - 1u) / kFinThreads, pad = m * kFinThreads - G;
 	// Horner over this thread's m consecutive spans (front-padded with zero spans: neutral)
 	uint32_t c = 0, s0 = 0, s1 = 0;
 	for (uint32_t i = 0; i < m; i++) {
@@ -293,9 +339,9 @@ __global__ __launch_bounds__(kThreads) void png_finish_kernel(const Vp8gEncDesc*
 	red[0][tid] = c;
 	red[1][tid] = s0;
 	red[2][tid] = s1;
-	for (int l = 0; l < kTreeLevels; l++) {
+	for (int l = 0; l < kFinLevels; l++) {
 		__syncthreads();
-		if (tid < (uint32_t)(kThreads >> (l + 1))) {
+		if (tid < (uint32_t)(kFinThreads >> (l + 1))) {
 			const uint32_t lo = tid << (l + 1), hi = lo + (1u << l);
 			red[0][lo] = op_apply(d.crc_ops[1 + l], red[0][lo]) ^ red[0][hi];
 			red[1][lo] = (red[1][lo] + red[1][hi]) % kMod;
@@ -401,11 +447,11 @@ PngOps png_ops(uint32_t G, uint32_t zend) {
 	auto it = g_ops.find({G, zend});
 	if (it != g_ops.end()) return it->second;
 	PngOps o;
-	const uint32_t m = (G + kThreads - 1u) / kThreads;
+	const uint32_t m = (G + kFinThreads - 1u) / kFinThreads;
 	Op zs = op_zeros(kSpan);
 	memcpy(o.ops[0], zs.c, 128);
 	Op zl = op_zeros((uint64_t)kSpan * m);
-	for (int l = 0; l < kTreeLevels; l++) {
+	for (int l = 0; l < kFinLevels; l++) {
 		memcpy(o.ops[1 + l], zl.c, 128);
 		zl = op_mul(zl, zl);
 	}
@@ -434,12 +480,12 @@ hipError_t tables_dev(uint32_t** out) {
 			for (int k = 0; k < 8; k++) c = (c & 1u) ? (c >> 1) ^ 0xEDB88320u : c >> 1;
 			t[b] = c;
 		}
-		for (int s = 1; s < 4; s++)
+		for (int s = 1; s < kSlice; s++)
 			for (uint32_t b = 0; b < 256; b++) t[256 * s + b] = (t[256 * (s - 1) + b] >> 8) ^ t[t[256 * (s - 1) + b] & 255u];
 		Op z = op_zeros(kPerThread);
 		for (int l = 0; l < kTreeLevels; l++, z = op_mul(z, z))
 			for (int j = 0; j < 8; j++)
-				for (uint32_t v = 0; v < 16; v++) t[1024 + l * 128 + j * 16 + v] = op_host_apply(z, v << (4 * j));
+				for (uint32_t v = 0; v < 16; v++) t[kNibBase + l * 128 + j * 16 + v] = op_host_apply(z, v << (4 * j));
 		uint32_t* p = nullptr;
 		e = hipMalloc((void**)&p, kTabWords * 4);
 		if (e != hipSuccess) return e;
@@ -547,13 +593,13 @@ VP8G_API int vp8g_encode_batch_device(const Vp8gEncDesc* h, const Vp8gEncDesc* d
 	hipError_t e = tables_dev(&tab);
 	if (e == hipSuccess) {
 		const int cus = vp8g::device_cus();
-		const uint32_t grid = min(total, (uint32_t)(cus > 0 ? cus : 256) * 12u);
+		const uint32_t grid = min(total, (uint32_t)(cus > 0 ? cus : 256) * 4u);
 		hipLaunchKernelGGL(enc_kernel, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, d_descs, n, total, d_src, d_out,
 		                   (uint32_t*)d_work, tab);
 		e = hipGetLastError();
 	}
 	if (e == hipSuccess && any_png) {
-		hipLaunchKernelGGL(png_finish_kernel, dim3(n), dim3(kThreads), 0, (hipStream_t)stream, d_descs, (const uint32_t*)d_work,
+		hipLaunchKernelGGL(png_finish_kernel, dim3(n), dim3(kFinThreads), 0, (hipStream_t)stream, d_descs, (const uint32_t*)d_work,
 		                   d_out, tab);
 		e = hipGetLastError();
 	}
