@@ -15,8 +15,10 @@ OFFLOAD_ARCH ?= gfx950
 
 HOST_SRC := $(PKG)/host/webp_riff.c $(PKG)/host/vp8_parse.c $(PKG)/host/vp8_synth.c
 HOST_HDR := $(PKG)/host/vp8_front.h $(PKG)/host/vp8_bool.h $(PKG)/host/vp8_tables.inc include/vp8g.h
-HIP_SRC := $(PKG)/csrc/vp8g_kernels.hip $(PKG)/csrc/vp8g_shim.hip $(PKG)/csrc/vp8g_rgb.hip
-HIP_HDR := $(PKG)/csrc/vp8g_device.h include/vp8g.h
+HIP_SRC := $(PKG)/csrc/vp8g_kernels.hip $(PKG)/csrc/vp8g_shim.hip $(PKG)/csrc/vp8g_rgb.hip $(PKG)/csrc/vp8g_pipeline.hip
+HIP_HDR := $(PKG)/csrc/vp8g_device.h include/vp8g.h $(PKG)/host/vp8_front.h
+# libvp8g links the host front end (the end-to-end batch path runs m05 on worker threads)
+HIP_LINK := -L$(LIB) -lvp8host -Wl,-rpath,'$$ORIGIN' -lpthread
 
 CFLAGS := -std=c11 -O3 -march=x86-64-v3 -Wall -Wextra -Wpedantic -fPIC -D_POSIX_C_SOURCE=200809L
 HIPFLAGS := -std=c++17 -O3 --offload-arch=$(OFFLOAD_ARCH) -fPIC -Wall -Wno-unused-function \
@@ -32,8 +34,8 @@ $(LIB) $(BIN):
 $(LIB)/libvp8host.so: $(HOST_SRC) $(HOST_HDR) | $(LIB)
 	$(CC) $(CFLAGS) -shared -Wl,-Bsymbolic -o $@ $(HOST_SRC)
 
-$(LIB)/libvp8g.so: $(HIP_SRC) $(HIP_HDR) | $(LIB)
-	$(HIPCC) $(HIPFLAGS) -shared -Wl,-Bsymbolic -o $@ $(HIP_SRC) -lpthread
+$(LIB)/libvp8g.so: $(HIP_SRC) $(HIP_HDR) $(LIB)/libvp8host.so | $(LIB)
+	$(HIPCC) $(HIPFLAGS) -shared -Wl,-Bsymbolic -o $@ $(HIP_SRC) $(HIP_LINK)
 
 $(BIN)/decoder: $(PKG)/host/decoder_main.c $(LIB)/libvp8host.so $(LIB)/libvp8g.so | $(BIN)
 	$(CC) $(CFLAGS) -o $@ $(PKG)/host/decoder_main.c -L$(LIB) -lvp8host -lvp8g -Wl,-rpath,'$$ORIGIN/../lib'
@@ -49,9 +51,9 @@ diag: $(foreach v,$(DIAG_VARIANTS),$(DIAG)/libvp8g_$(v).so)
 $(DIAG):
 	mkdir -p $@
 $(DIAG)/libvp8g_stamps.so: $(HIP_SRC) $(HIP_HDR) | $(DIAG)
-	$(HIPCC) $(HIPFLAGS) -DVP8G_STAMPS -shared -Wl,-Bsymbolic -o $@ $(HIP_SRC) -lpthread
+	$(HIPCC) $(HIPFLAGS) -DVP8G_STAMPS -shared -Wl,-Bsymbolic -o $@ $(HIP_SRC) -L$(LIB) -lvp8host -Wl,-rpath,'$$ORIGIN/..' -lpthread
 $(DIAG)/libvp8g_abl%.so: $(HIP_SRC) $(HIP_HDR) | $(DIAG)
-	$(HIPCC) $(HIPFLAGS) -DVP8G_ABLATE=$* -shared -Wl,-Bsymbolic -o $@ $(HIP_SRC) -lpthread
+	$(HIPCC) $(HIPFLAGS) -DVP8G_ABLATE=$* -shared -Wl,-Bsymbolic -o $@ $(HIP_SRC) -L$(LIB) -lvp8host -Wl,-rpath,'$$ORIGIN/..' -lpthread
 
 clean:
 	rm -rf $(LIB) $(BIN)

@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
+    ap.add_argument("--e2e-frames", type=int, default=96,
+                    help="frames of the end-to-end object (.webp bytes -> I420, vp8g_decode_webp_batch); 0 = off")
     ap.add_argument("--encode", default="png", choices=["none", "rgb", "ppm", "png"],
                     help="also time the m08/m09 stage on the batch's output (secondary object 'encode')")
     return ap.parse_args()
@@ -147,6 +149,52 @@ class EncodeStage:
     def file(self, i: int) -> bytes:
         o = self.outs[i]
         return self.out[o:o + self.file_len].cpu().numpy().tobytes()
+
+
+def end_to_end(manifest, n_frames, filtered, threads):
+    """SURVEY §8(f1) step 1 + §8(f2): whole decode from .webp bytes in host memory to I420 in host
+    memory (vp8g_decode_webp_batch: threaded host m05 into the packed format, device expansion +
+    recon(+LF), D2H), wall clock of one call; next to it the reference's own `decoder -yuvf`
+    (oracle/_ref/decoder, one process per frame, `threads` at a time) on a sample of the same files."""
+    files = [(ROOT / "tests" / "fixtures" / r).read_bytes() for r in FIXTURES]
+    batch = [files[i % 4] for i in range(n_frames)]
+    vp8g.gpu_decode_webp_batch(batch[:8], filtered, threads)  # warm: device buffers, code objects
+    t = time.perf_counter()
+    outs, st = vp8g.gpu_decode_webp_batch(batch, filtered, threads)
+    dt = time.perf_counter() - t
+    key = "yuvf_sha256" if filtered else "yuv_sha256"
+    ok = all(s == 0 for s in st) and all(hashlib.sha256(outs[i]).hexdigest() == manifest["files"][FIXTURES[i % 4]][key]
+                                         for i in range(min(8, n_frames)))
+    mp = n_frames * 3840 * 2160 / 1e6
+    obj = {"stage": "end to end: .webp bytes in host memory -> I420 in host memory (container, header, m05 on host "
+                    "threads into the packed format; upload, expansion, recon+LF on the device; D2H)",
+           "value": round(mp / dt, 1), "unit": "MP/s", "frames": n_frames, "threads": threads,
+           "seconds": round(dt, 3), "parity": "bit-exact vs reference (8 frames sha256)" if ok else "MISMATCH",
+           "reference_cli": None}
+    dec = ROOT / "oracle" / "_ref" / "decoder"
+    if dec.exists():
+        import subprocess
+        import tempfile
+        from concurrent.futures import ThreadPoolExecutor
+        n_ref = 2 * threads
+        with tempfile.TemporaryDirectory() as td:
+            src = [pathlib.Path(td) / f"f{i}.webp" for i in range(4)]
+            for i in range(4):
+                src[i].write_bytes(files[i])
+            def one(i):
+                r = subprocess.run([str(dec), "-yuvf" if filtered else "-yuv", str(src[i % 4]), str(pathlib.Path(td) / f"o{i}.yuv")],
+                                   capture_output=True)
+                (pathlib.Path(td) / f"o{i}.yuv").unlink(missing_ok=True)
+                return r.returncode
+            t = time.perf_counter()
+            with ThreadPoolExecutor(threads) as ex:
+                rcs = list(ex.map(one, range(n_ref)))
+            rdt = time.perf_counter() - t
+        if all(rc == 0 for rc in rcs):
+            obj["reference_cli"] = {"value": round(n_ref * 3840 * 2160 / 1e6 / rdt, 1), "unit": "MP/s", "cores": threads,
+                                    "sample": f"{n_ref} x `decoder -yuvf` (reference, one process per frame, {threads} at a "
+                                              f"time), {rdt:.1f} s"}
+    return obj
 
 
 def cpu_baseline(frames, filtered, threads, seconds):
@@ -267,6 +315,10 @@ def main():
                                 "frac": round(enc_gbs / PEAK_HBM_GBS, 4),
                                 "algorithmic_bytes_per_launch": enc.bytes}}
 
+    e2e = None
+    if rank == 0 and world == 1 and args.e2e_frames > 0:
+        e2e = end_to_end(manifest, args.e2e_frames, filtered, args.cpu_threads)
+
     stamp_shares = None
     if stamps:
         acc = (C.c_ulonglong * 16)()
@@ -308,6 +360,8 @@ def main():
         }
         if enc_obj:
             line["encode"] = enc_obj
+        if e2e:
+            line["end_to_end"] = e2e
         if stamp_shares:
             line["stamps"] = stamp_shares
         print(json.dumps(line), flush=True)

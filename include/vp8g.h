@@ -207,6 +207,32 @@ int vp8g_decode_batch_device(const Vp8gFrameDesc* h_descs, const Vp8gFrameDesc* 
 int vp8g_reconstruct_batch(const Vp8KeyFrameHeader* const* kfs, const Vp8DecodedFrame* const* frames, uint32_t n,
                            int filtered, Yuv420Image* outs);
 
+/* ---- End-to-end batch path: .webp bytes -> I420 (SURVEY §8(f1) step 1 + §8(f2)) ---------- */
+
+/* Packed m05 output, the host -> device wire format.  Per MB the 25 blocks (Y 0..15, U 0..3,
+ * V 0..3, Y2) each leave a 16-bit mask of the natural positions holding a non-zero coefficient;
+ * the values follow block by block, natural order within a block.  A 4K frame of the bench
+ * fixtures packs to ~2.5-5 MB instead of the 26.6 MB of dense int16 arrays. */
+#define VP8G_PK_BLOCKS 25
+typedef struct {
+	Vp8KeyFrameHeader kf;
+	Vp8DecodedFrame f;  /* header fields, side arrays and stats; coeff_* are NULL */
+	uint16_t* masks;    /* [mb_total * 25] */
+	uint32_t* mb_off;   /* [mb_total] index of the MB's first value in values[] */
+	int16_t* values;    /* [n_values] */
+	uint64_t n_values;
+} Vp8gPackedFrame;
+
+/* Decode n .webp file images end to end: container/header/m05 on `threads` host threads (0 = the
+ * CPUs this process may run on) into the packed format, chunks of frames uploaded packed,
+ * expanded and reconstructed (+ loop filter when `filtered`) on the device while the next chunk
+ * is being entropy-decoded, I420 downloaded into outs[i] (yuv420_alloc layout; the caller frees
+ * each with yuv420_free).  status[i] (may be NULL) = 0 or the errno of frame i's failure (its
+ * image is left zeroed).  Returns 0 when every frame decoded, else -1 + errno of the first
+ * failing frame (EIO for a device failure, in which case no image is returned). */
+int vp8g_decode_webp_batch(const ByteSpan* files, uint32_t n, int filtered, uint32_t threads, Yuv420Image* outs,
+                           int* status);
+
 /* ---- m08 / m09 boundary: I420 -> RGB24 ("fancy" 4:2:0 upsampling) and the file writers -- */
 
 /* replaces src/m08_yuv2rgb_ppm/yuv2rgb_ppm.c:123 (decl yuv2rgb_ppm.h:10): binary PPM (P6) of img
@@ -268,7 +294,7 @@ int vp8g_encode_batch_device(const Vp8gEncDesc* h_descs, const Vp8gEncDesc* d_de
 const char* vp8g_last_error(void);
 
 /* ABI version of this header (bumped on any layout change). */
-#define VP8G_ABI_VERSION 2
+#define VP8G_ABI_VERSION 3
 uint32_t vp8g_abi_version(void);
 
 #ifdef __cplusplus

@@ -65,6 +65,15 @@ uint32_t pick_split(uint32_t split_hint, uint32_t n_frames, uint32_t nw, uint32_
 // waves_hint if non-zero, else 8, or 16 when n_frames <= the device's CU count.
 uint32_t pick_waves(uint32_t waves_hint, uint32_t max_mb_rows, uint32_t n_frames);
 
+// vp8g_make_frame_desc; dense_coeffs = false skips the check of the coeff_* pointers (packed
+// frames: the coefficients reach the device through the expansion kernel).
+int make_desc(const Vp8KeyFrameHeader* kf, const Vp8DecodedFrame* d, int filtered, uint64_t mb_offset, uint64_t out_offset,
+              Vp8gFrameDesc* out, bool dense_coeffs);
+
+// Planes in the yuv420_alloc layout; init = false leaves them uninitialised (outputs a D2H
+// overwrites completely).
+int alloc_planes(Yuv420Image* img, uint32_t width, uint32_t height, bool init);
+
 // Record a HIP failure for vp8g_last_error() (calling thread).
 void set_error_text(const char* where, hipError_t e);
 

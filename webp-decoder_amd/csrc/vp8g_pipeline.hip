@@ -1,0 +1,402 @@
+// vp8g_pipeline.hip -- end-to-end batch decode, .webp bytes -> I420 in host memory
+// (vp8g_decode_webp_batch, include/vp8g.h).
+//
+//   worker threads   container + key-frame header + m05 (host/vp8_parse.c, reentrant) into the
+//                    packed wire format, frames handed out in order from an atomic counter and
+//                    kept at most a window ahead of the device
+//   this thread      groups finished frames into chunks; per chunk: H2D of the side arrays, the
+//                    block masks and the non-zero values (~5x less than dense int16), expansion
+//                    to the dense SoA the recon kernel reads, the fused recon(+LF) kernel, D2H
+//                    into the callers' images.  Two chunk slots alternate, so the device work and
+//                    the copies of one chunk overlap the entropy decoding of the next ones.
+//
+// The reference decodes one file per process (src/main.c:591-705: m01..m05 then m06/m07); its
+// m05 keeps global state (vp8_tokens.c:382, :625), which is why it cannot be threaded as is.
+#include <errno.h>
+#include <sched.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../host/vp8_front.h"
+#include "vp8g_device.h"
+
+#define VP8G_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+constexpr uint32_t kChunkFrames = 64;          // frames per device chunk (at most)
+constexpr uint64_t kChunkMbs = 2u << 20;       // macroblocks per chunk (at most, unless one frame is bigger)
+constexpr uint32_t kNb = VP8G_PK_BLOCKS;
+
+// Packed -> dense coefficients.  32 lanes per MB; lane b < 25 owns block b (Y 0..15, U 0..3,
+// V 0..3, Y2).  Its values start at the MB's offset plus the popcounts of the blocks before it
+// (a 32-lane inclusive scan); position i takes value rank popcount(mask & ((1 << i) - 1)).
+__global__ __launch_bounds__(256) void expand_kernel(const uint16_t* __restrict__ masks, const uint32_t* __restrict__ mb_off,
+                                                     const int16_t* __restrict__ vals, uint32_t n_mb, int16_t* __restrict__ cy,
+                                                     int16_t* __restrict__ cu, int16_t* __restrict__ cv,
+                                                     int16_t* __restrict__ cy2) {
+	const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+	const uint32_t mb = t >> 5, b = t & 31u;
+	if (mb >= n_mb) return;  // whole 32-lane groups leave together
+	const uint32_t m = b < kNb ? masks[(size_t)mb * kNb + b] : 0u;
+	const uint32_t cnt = __popc(m);
+	uint32_t incl = cnt;
+#pragma unroll
+	for (int d = 1; d < 32; d <<= 1) {
+		const uint32_t v = __shfl_up(incl, (unsigned)d, 32);
+		if (b >= (uint32_t)d) incl += v;
+	}
+	if (b >= kNb) return;
+	const int16_t* src = vals + mb_off[mb] + (incl - cnt);
+	uint32_t w[8];
+#pragma unroll
+	for (int i = 0; i < 8; i++) {
+		const uint32_t k0 = 2 * i, k1 = 2 * i + 1;
+		uint32_t lo = 0, hi = 0;
+		if ((m >> k0) & 1u) lo = (uint16_t)src[__popc(m & ((1u << k0) - 1u))];
+		if ((m >> k1) & 1u) hi = (uint16_t)src[__popc(m & ((1u << k1) - 1u))];
+		w[i] = lo | (hi << 16);
+	}
+	int16_t* dst = b < 16u   ? cy + ((size_t)mb * 16u + b) * 16u
+	               : b < 20u ? cu + ((size_t)mb * 4u + (b - 16u)) * 16u
+	               : b < 24u ? cv + ((size_t)mb * 4u + (b - 20u)) * 16u
+	                         : cy2 + (size_t)mb * 16u;
+	uint4* d4 = (uint4*)dst;
+	d4[0] = make_uint4(w[0], w[1], w[2], w[3]);
+	d4[1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+
+inline uint64_t al256(uint64_t x) { return (x + 255u) & ~(uint64_t)255u; }
+
+uint32_t default_threads() {
+	cpu_set_t set;
+	if (sched_getaffinity(0, sizeof(set), &set) == 0) {
+		const int n = CPU_COUNT(&set);
+		if (n > 0) return (uint32_t)n;
+	}
+	const unsigned h = std::thread::hardware_concurrency();
+	return h ? h : 1u;
+}
+
+// Frames handed from the workers to the device thread.
+struct Feed {
+	const ByteSpan* files = nullptr;
+	uint32_t n = 0;
+	std::vector<Vp8gPackedFrame> pk;
+	std::vector<int> err;
+	std::unique_ptr<uint8_t[]> ready;
+	std::atomic<uint32_t> next{0};
+	uint32_t limit = 0;  // workers may start frames < limit (guarded by mu)
+	bool abort = false;
+	std::mutex mu;
+	std::condition_variable cv_ready, cv_limit;
+
+	void work() {
+		for (;;) {
+			const uint32_t i = next.fetch_add(1);
+			if (i >= n) return;
+			{
+				std::unique_lock<std::mutex> lk(mu);
+				cv_limit.wait(lk, [&] { return i < limit || abort; });
+				if (abort) return;
+			}
+			int stage = 0, e = 0;
+			if (!files[i].data) e = EINVAL;
+			else if (vp8f_decode_packed_memory(files[i].data, files[i].size, &pk[i], &stage, 0) != 0) e = errno ? errno : EINVAL;
+			{
+				std::lock_guard<std::mutex> lk(mu);
+				err[i] = e;
+				ready[i] = 1;
+			}
+			cv_ready.notify_all();
+		}
+	}
+	void wait_ready(uint32_t i) {
+		std::unique_lock<std::mutex> lk(mu);
+		cv_ready.wait(lk, [&] { return ready[i] != 0; });
+	}
+	void set_limit(uint32_t l) {
+		{
+			std::lock_guard<std::mutex> lk(mu);
+			if (l > limit) limit = l;
+		}
+		cv_limit.notify_all();
+	}
+	void stop() {
+		{
+			std::lock_guard<std::mutex> lk(mu);
+			abort = true;
+		}
+		cv_limit.notify_all();
+	}
+};
+
+// One chunk's device buffer and the host state that must live until its copies are done.
+struct Slot {
+	uint8_t* buf = nullptr;
+	size_t cap = 0;
+	hipEvent_t done = nullptr;
+	bool busy = false;
+	std::vector<uint32_t> frames;  // frame indices of the chunk (packed data freed when the slot is reused)
+	std::vector<Vp8gFrameDesc> descs;
+	uint32_t status = 0;
+};
+
+struct ChunkLayout {
+	uint64_t ym, uvm, seg, hasc, bm, masks, mboff, vals, cy, cu, cv, cy2, desc, status, gctx, mbox, gprog, out, total;
+};
+
+hipError_t grow(Slot& s, size_t need) {
+	if (need <= s.cap) return hipSuccess;
+	if (s.buf) (void)hipFree(s.buf);
+	s.buf = nullptr;
+	s.cap = 0;
+	const size_t n = need + need / 4;
+	hipError_t e = hipMalloc((void**)&s.buf, n);
+	if (e == hipSuccess) s.cap = n;
+	return e;
+}
+
+}  // namespace
+
+VP8G_API int vp8g_decode_webp_batch(const ByteSpan* files, uint32_t n, int filtered, uint32_t threads, Yuv420Image* outs,
+                                    int* status) {
+	if (!files || !outs || n == 0) {
+		errno = EINVAL;
+		return -1;
+	}
+	for (uint32_t i = 0; i < n; i++) memset(&outs[i], 0, sizeof(outs[i]));
+	if (!threads) threads = default_threads();
+	if (threads > n) threads = n;
+
+	Feed feed;
+	feed.files = files;
+	feed.n = n;
+	feed.pk.assign(n, Vp8gPackedFrame{});
+	feed.err.assign(n, 0);
+	feed.ready.reset(new uint8_t[n]());
+	const uint32_t window = 2 * kChunkFrames > 4 * threads ? 2 * kChunkFrames : 4 * threads;
+	feed.limit = window;
+	std::vector<std::thread> pool;
+	pool.reserve(threads);
+	for (uint32_t t = 0; t < threads; t++) pool.emplace_back([&feed] { feed.work(); });
+
+	hipStream_t stream = nullptr;
+	Slot slots[2];
+	uint32_t released = 0;  // frames whose packed data is freed (all below this index)
+	const char* where = nullptr;
+	hipError_t he = hipSuccess;
+	auto release = [&](Slot& s) {
+		for (uint32_t i : s.frames) vp8f_packed_free(&feed.pk[i]);
+		s.frames.clear();
+	};
+	auto finish_slot = [&](Slot& s) -> bool {  // wait for a slot's chunk; false on a device failure
+		if (!s.busy) return true;
+		s.busy = false;
+		if ((he = hipEventSynchronize(s.done)) != hipSuccess) {
+			where = "sync";
+			return false;
+		}
+		release(s);
+		if (s.status != 0) {
+			where = "kernel status";
+			he = hipErrorLaunchFailure;
+			return false;
+		}
+		return true;
+	};
+
+#define PTRY(expr, w)                \
+	do {                             \
+		if ((he = (expr)) != hipSuccess) { \
+			where = w;               \
+			goto fail;               \
+		}                            \
+	} while (0)
+
+	PTRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "stream");
+	for (Slot& s : slots) PTRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), "event");
+
+	{
+		uint32_t a = 0, chunk = 0;
+		while (a < n) {
+			// -- gather the next chunk: consecutive frames, in order, as they finish
+			std::vector<uint32_t> idx;
+			uint64_t mbs = 0, vals = 0, outb = 0;
+			uint32_t b = a, max_cols = 0, max_rows = 0;
+			while (b < n && b - a < kChunkFrames) {
+				feed.wait_ready(b);
+				if (feed.err[b] == 0) {
+					const Vp8DecodedFrame& f = feed.pk[b].f;
+					if (!idx.empty() && mbs + f.mb_total > kChunkMbs) break;
+					idx.push_back(b);
+					mbs += f.mb_total;
+					vals += feed.pk[b].n_values;
+					outb = al256(outb + vp8g_i420_size(feed.pk[b].kf.width, feed.pk[b].kf.height));
+					if (f.mb_cols > max_cols) max_cols = f.mb_cols;
+					if (f.mb_rows > max_rows) max_rows = f.mb_rows;
+				}
+				b++;
+			}
+			Slot& s = slots[chunk & 1];
+			if (!finish_slot(s)) goto fail;
+			if (idx.empty()) {
+				a = b;
+				continue;
+			}
+			const uint32_t nf = (uint32_t)idx.size();
+			// -- launch geometry (the choices vp8g_reconstruct_batch makes)
+			uint32_t nw = vp8g::pick_waves(0, max_rows, nf);
+			if (vp8g::pick_split(0, nf, 8, max_rows) > 1) nw = 8;
+			const bool big = vp8g::lds_bytes((int)nw, max_cols, false) > (size_t)vp8g::kMaxLds;
+			const uint32_t k = big ? 1u : vp8g::pick_split(0, nf, nw, max_rows);
+			ChunkLayout L;
+			uint64_t o = 0;
+			L.ym = o, o = al256(o + mbs);
+			L.uvm = o, o = al256(o + mbs);
+			L.seg = o, o = al256(o + mbs);
+			L.hasc = o, o = al256(o + mbs);
+			L.bm = o, o = al256(o + mbs * 16);
+			L.masks = o, o = al256(o + mbs * kNb * 2);
+			L.mboff = o, o = al256(o + mbs * 4);
+			L.vals = o, o = al256(o + vals * 2 + 64);  // +64: the expansion may address one past the end
+			L.cy = o, o = al256(o + mbs * 512);
+			L.cu = o, o = al256(o + mbs * 128);
+			L.cv = o, o = al256(o + mbs * 128);
+			L.cy2 = o, o = al256(o + mbs * 32);
+			L.desc = o, o = al256(o + nf * sizeof(Vp8gFrameDesc));
+			L.status = o, o = al256(o + 4);
+			L.gctx = o, o = al256(o + (big ? (uint64_t)nf * max_cols * vp8g::kCtxBytesPerCol : 0));
+			L.mbox = o, o = al256(o + (k > 1 ? (uint64_t)nf * k * max_cols * vp8g::kCtxBytesPerCol : 0));
+			L.gprog = o, o = al256(o + (k > 1 ? (uint64_t)nf * k * 4 : 0));
+			L.out = o, o = al256(o + outb);
+			L.total = o;
+			PTRY(grow(s, L.total), "hipMalloc(chunk)");
+			uint8_t* d = s.buf;
+			// -- descriptors and output images
+			s.descs.assign(nf, Vp8gFrameDesc{});
+			{
+				uint64_t mo = 0, vo = 0, oo = 0;
+				for (uint32_t j = 0; j < nf; j++) {
+					Vp8gPackedFrame& p = feed.pk[idx[j]];
+					if (vp8g::make_desc(&p.kf, &p.f, filtered, mo, oo, &s.descs[j], false) != 0 ||
+					    vp8g::alloc_planes(&outs[idx[j]], p.kf.width, p.kf.height, false) != 0) {
+						feed.err[idx[j]] = errno ? errno : EINVAL;  // (cannot happen for a frame m05 accepted)
+						s.descs[j].flags = 0;
+					}
+					// chunk-relative value offsets
+					if (vo)
+						for (uint32_t m = 0; m < p.f.mb_total; m++) p.mb_off[m] += (uint32_t)vo;
+					const uint64_t mt = p.f.mb_total;
+					PTRY(hipMemcpyAsync(d + L.ym + mo, p.f.ymode, mt, hipMemcpyHostToDevice, stream), "H2D");
+					PTRY(hipMemcpyAsync(d + L.uvm + mo, p.f.uv_mode, mt, hipMemcpyHostToDevice, stream), "H2D");
+					PTRY(hipMemcpyAsync(d + L.seg + mo, p.f.segment_id, mt, hipMemcpyHostToDevice, stream), "H2D");
+					PTRY(hipMemcpyAsync(d + L.hasc + mo, p.f.has_coeff, mt, hipMemcpyHostToDevice, stream), "H2D");
+					PTRY(hipMemcpyAsync(d + L.bm + mo * 16, p.f.bmode, mt * 16, hipMemcpyHostToDevice, stream), "H2D");
+					PTRY(hipMemcpyAsync(d + L.masks + mo * kNb * 2, p.masks, mt * kNb * 2, hipMemcpyHostToDevice, stream), "H2D");
+					PTRY(hipMemcpyAsync(d + L.mboff + mo * 4, p.mb_off, mt * 4, hipMemcpyHostToDevice, stream), "H2D");
+					if (p.n_values)
+						PTRY(hipMemcpyAsync(d + L.vals + vo * 2, p.values, p.n_values * 2, hipMemcpyHostToDevice, stream), "H2D");
+					mo += mt;
+					vo += p.n_values;
+					oo = al256(oo + vp8g_i420_size(p.kf.width, p.kf.height));
+				}
+			}
+			s.frames = idx;
+			PTRY(hipMemcpyAsync(d + L.desc, s.descs.data(), nf * sizeof(Vp8gFrameDesc), hipMemcpyHostToDevice, stream), "H2D");
+			PTRY(hipMemsetAsync(d + L.status, 0, 4, stream), "memset");
+			if (k > 1) PTRY(hipMemsetAsync(d + L.gprog, 0, (size_t)nf * k * 4, stream), "memset");
+			// -- expansion + recon(+LF)
+			{
+				const uint64_t threads_x = mbs * 32;
+				hipLaunchKernelGGL(expand_kernel, dim3((uint32_t)((threads_x + 255) / 256)), dim3(256), 0, stream,
+				                   (const uint16_t*)(d + L.masks), (const uint32_t*)(d + L.mboff), (const int16_t*)(d + L.vals),
+				                   (uint32_t)mbs, (int16_t*)(d + L.cy), (int16_t*)(d + L.cu), (int16_t*)(d + L.cv),
+				                   (int16_t*)(d + L.cy2));
+				PTRY(hipGetLastError(), "expand launch");
+				Vp8gBatchArrays arr;
+				arr.coeff_y = (const int16_t*)(d + L.cy);
+				arr.coeff_u = (const int16_t*)(d + L.cu);
+				arr.coeff_v = (const int16_t*)(d + L.cv);
+				arr.coeff_y2 = (const int16_t*)(d + L.cy2);
+				arr.ymode = d + L.ym;
+				arr.uv_mode = d + L.uvm;
+				arr.segment_id = d + L.seg;
+				arr.has_coeff = d + L.hasc;
+				arr.bmode = d + L.bm;
+				arr.src = nullptr;
+				arr.status = (uint32_t*)(d + L.status);
+				PTRY(vp8g::launch_frames((const Vp8gFrameDesc*)(d + L.desc), nf, arr, d + L.out, max_cols, max_rows,
+				                         big ? d + L.gctx : nullptr, stream, nw, k, k > 1 ? d + L.mbox : nullptr,
+				                         k > 1 ? (uint32_t*)(d + L.gprog) : nullptr),
+				     "recon launch");
+			}
+			// -- D2H into the callers' images
+			for (uint32_t j = 0; j < nf; j++) {
+				const Vp8gFrameDesc& fd = s.descs[j];
+				Yuv420Image& img = outs[idx[j]];
+				if (!img.y) continue;
+				const size_t ysz = (size_t)fd.stride_y * fd.height, uvsz = (size_t)fd.stride_uv * ((fd.height + 1) / 2);
+				PTRY(hipMemcpyAsync(img.y, d + L.out + fd.out_y, ysz, hipMemcpyDeviceToHost, stream), "D2H");
+				PTRY(hipMemcpyAsync(img.u, d + L.out + fd.out_u, uvsz, hipMemcpyDeviceToHost, stream), "D2H");
+				PTRY(hipMemcpyAsync(img.v, d + L.out + fd.out_v, uvsz, hipMemcpyDeviceToHost, stream), "D2H");
+			}
+			PTRY(hipMemcpyAsync(&s.status, d + L.status, 4, hipMemcpyDeviceToHost, stream), "D2H");
+			PTRY(hipEventRecord(s.done, stream), "event");
+			s.busy = true;
+			released = b;
+			feed.set_limit(released + window);
+			a = b;
+			chunk++;
+		}
+		for (Slot& s : slots)
+			if (!finish_slot(s)) goto fail;
+	}
+	for (auto& t : pool) t.join();
+	pool.clear();
+	for (Slot& s : slots) {
+		if (s.done) (void)hipEventDestroy(s.done);
+		if (s.buf) (void)hipFree(s.buf);
+	}
+	(void)hipStreamDestroy(stream);
+	{
+		int first = 0;
+		for (uint32_t i = 0; i < n; i++) {
+			vp8f_packed_free(&feed.pk[i]);  // failed frames (the others were freed per chunk)
+			if (status) status[i] = feed.err[i];
+			if (feed.err[i] && !first) first = feed.err[i];
+			if (feed.err[i]) yuv420_free(&outs[i]);
+		}
+		if (first) {
+			errno = first;
+			return -1;
+		}
+	}
+	return 0;
+
+fail:
+	feed.stop();
+	for (auto& t : pool) t.join();
+	if (stream) (void)hipStreamSynchronize(stream);
+	vp8g::set_error_text(where ? where : "pipeline", he);
+	for (Slot& s : slots) {
+		if (s.done) (void)hipEventDestroy(s.done);
+		if (s.buf) (void)hipFree(s.buf);
+	}
+	if (stream) (void)hipStreamDestroy(stream);
+	for (uint32_t i = 0; i < n; i++) {
+		vp8f_packed_free(&feed.pk[i]);
+		yuv420_free(&outs[i]);
+		if (status) status[i] = EIO;
+	}
+	errno = EIO;
+	return -1;
+#undef PTRY
+}

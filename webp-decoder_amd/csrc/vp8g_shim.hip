@@ -227,13 +227,13 @@ int run_locked(const std::vector<Vp8gFrameDesc>& descs, const Vp8gBatchArrays& a
 // Reference entry points
 // ---------------------------------------------------------------------------------------------
 
-// Planes as yuv420_alloc lays them out, left uninitialised: for outputs the D2H overwrites
-// completely (the fill of yuv420_alloc would be a second full pass over fresh pages).
-int alloc_planes(Yuv420Image* img, uint32_t width, uint32_t height, bool init);
+VP8G_API int yuv420_alloc(Yuv420Image* img, uint32_t width, uint32_t height) {
+	return vp8g::alloc_planes(img, width, height, true);
+}
 
-VP8G_API int yuv420_alloc(Yuv420Image* img, uint32_t width, uint32_t height) { return alloc_planes(img, width, height, true); }
-
-int alloc_planes(Yuv420Image* img, uint32_t width, uint32_t height, bool init) {
+// Planes as yuv420_alloc lays them out; init = false leaves them uninitialised, for outputs the
+// D2H overwrites completely (the fill would be a second full pass over fresh pages).
+int vp8g::alloc_planes(Yuv420Image* img, uint32_t width, uint32_t height, bool init) {
 	if (!img || width == 0 || height == 0) {
 		errno = EINVAL;
 		return -1;
@@ -277,7 +277,13 @@ VP8G_API uint64_t vp8g_i420_size(uint32_t w, uint32_t h) {
 
 VP8G_API int vp8g_make_frame_desc(const Vp8KeyFrameHeader* kf, const Vp8DecodedFrame* d, int filtered, uint64_t mb_offset,
                                   uint64_t out_offset, Vp8gFrameDesc* out) {
-	if (!out || !frame_ok(d)) {
+	return vp8g::make_desc(kf, d, filtered, mb_offset, out_offset, out, true);
+}
+
+int vp8g::make_desc(const Vp8KeyFrameHeader* kf, const Vp8DecodedFrame* d, int filtered, uint64_t mb_offset,
+                    uint64_t out_offset, Vp8gFrameDesc* out, bool dense_coeffs) {
+	if (!out || !d || !d->mb_cols || !d->mb_rows || d->mb_cols > 1024 || d->mb_rows > 1024 ||
+	    (uint64_t)d->mb_cols * d->mb_rows != d->mb_total || (dense_coeffs && !frame_ok(d))) {
 		errno = EINVAL;
 		return -1;
 	}
@@ -331,7 +337,7 @@ VP8G_API int vp8g_reconstruct_batch(const Vp8KeyFrameHeader* const* kfs, const V
 		outb = align256(outb + vp8g_i420_size(kfs[i]->width, kfs[i]->height));
 	}
 	for (uint32_t i = 0; i < n; i++) {
-		if (alloc_planes(&outs[i], kfs[i]->width, kfs[i]->height, false) != 0) {
+		if (vp8g::alloc_planes(&outs[i], kfs[i]->width, kfs[i]->height, false) != 0) {
 			for (uint32_t k = 0; k < i; k++) yuv420_free(&outs[k]);
 			return -1;
 		}

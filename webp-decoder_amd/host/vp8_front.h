@@ -42,6 +42,16 @@ int vp8f_decode_file(const char* path, Vp8KeyFrameHeader* kf, Vp8DecodedFrame* o
 /* Same for an in-memory file image. */
 int vp8f_decode_memory(const uint8_t* data, size_t size, Vp8KeyFrameHeader* kf, Vp8DecodedFrame* out, int* stage);
 
+/* m05 into the packed wire format (Vp8gPackedFrame, include/vp8g.h): same
+ * decode, side arrays and stats as vp8_decode_decoded_frame, but each 4x4 block leaves only its
+ * non-zero mask and values (no dense coefficient arrays).  The FNV coefficient hash is computed
+ * only with VP8F_PACK_HASH (stats.coeff_hash_fnv1a64 = 0 otherwise).  Reentrant. */
+#define VP8F_PACK_HASH 1u
+int vp8f_decode_packed(ByteSpan vp8_payload, Vp8gPackedFrame* out, unsigned flags);
+/* container + key-frame header + vp8f_decode_packed; stage codes as vp8f_decode_file */
+int vp8f_decode_packed_memory(const uint8_t* data, size_t size, Vp8gPackedFrame* out, int* stage, unsigned flags);
+void vp8f_packed_free(Vp8gPackedFrame* p);
+
 /* Seeded synthetic Vp8DecodedFrame (build-defined generator, see vp8_synth.c header for the
  * exact distribution).  profile 0 = "measured-like" statistics, 1 = stress (full-range coeffs,
  * all modes uniformly, random LF/segment parameters).  kf receives width/height. */

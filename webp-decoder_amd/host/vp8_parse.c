@@ -95,13 +95,14 @@ static void note_overread(TokenCtx* t, uint32_t mb, uint32_t plane, uint32_t blk
 	st->token_overread_stage = stage;
 }
 
-/* Decodes one 4x4 block's tokens (RFC 6386 13).  Returns 1 if some value is non-zero.
+/* Decodes one 4x4 block's tokens (RFC 6386 13) into out[] (natural order).  Returns the mask of
+ * natural positions holding a non-zero value (the block "has coefficients" iff it is non-zero).
  * `plane_tag` is only for the overread diagnostics (0=Y 1=Y2 2=U 3=V). */
-static int read_block(TokenCtx* t, int type, int first, int ctx, int16_t out[16], uint32_t mb, uint32_t plane_tag,
-                      uint32_t blk) {
+static uint32_t read_block(TokenCtx* t, int type, int first, int ctx, int16_t out[16], uint32_t mb, uint32_t plane_tag,
+                           uint32_t blk) {
 	Vp8CoeffStats* st = t->st;
 	memset(out, 0, 16 * sizeof(int16_t));
-	int nonzero = 0;
+	uint32_t mask = 0;
 	int after_zero = 0;
 	for (int pos = first; pos < 16; pos++) {
 		const uint8_t* p = t->probs[type][k_band[pos]][ctx];
@@ -123,18 +124,48 @@ static int read_block(TokenCtx* t, int type, int first, int ctx, int16_t out[16]
 			int neg = vp8b_read(&t->tok, 128);
 			note_overread(t, mb, plane_tag, blk, (uint32_t)pos, 2);
 			out[k_scan[pos]] = (int16_t)(neg ? -mag : mag);
-			nonzero = 1;
+			mask |= 1u << k_scan[pos];
 			st->coeff_nonzero_total++;
 			if ((uint32_t)mag > st->coeff_abs_max) st->coeff_abs_max = (uint32_t)mag;
 		}
 		ctx = mag == 0 ? 0 : (mag == 1 ? 1 : 2);
 		after_zero = (tok == TOK_ZERO);
 	}
-	return nonzero;
+	return mask;
+}
+
+/* Where decoded blocks go: the dense Vp8DecodedFrame arrays (the reference's m05 output), or the
+ * packed wire format (Vp8gPackedFrame: one non-zero mask per block + the non-zero values). */
+typedef struct {
+	Vp8gPackedFrame* pk; /* NULL: dense */
+	int hash;            /* fold every block into the FNV-1a coefficient hash */
+	size_t cap;          /* packed: capacity of pk->values */
+} Sink;
+
+static int sink_values(Sink* s, uint32_t mb, uint32_t bi, const int16_t* blk, uint32_t mask) {
+	Vp8gPackedFrame* pk = s->pk;
+	pk->masks[(size_t)mb * VP8G_PK_BLOCKS + bi] = (uint16_t)mask;
+	if (pk->n_values + 16 > s->cap) {
+		size_t nc = s->cap * 2 + 1024;
+		int16_t* nv = (int16_t*)realloc(pk->values, nc * sizeof(int16_t));
+		if (!nv) {
+			errno = ENOMEM;
+			return -1;
+		}
+		pk->values = nv;
+		s->cap = nc;
+	}
+	int16_t* v = pk->values + pk->n_values;
+	while (mask) {
+		*v++ = blk[__builtin_ctz(mask)];
+		mask &= mask - 1u;
+	}
+	pk->n_values = (uint64_t)(v - pk->values);
+	return 0;
 }
 
 /* Per-MB token decode over the whole frame (RFC 6386 13, reference vp8_tokens.c:354-622). */
-static int read_all_tokens(TokenCtx* t, Vp8DecodedFrame* f, const uint8_t* has_y2) {
+static int read_all_tokens(TokenCtx* t, Vp8DecodedFrame* f, const uint8_t* has_y2, Sink* sk) {
 	const uint32_t cols = f->mb_cols;
 	uint8_t* above = (uint8_t*)calloc((size_t)cols, 9); /* per MB column: Y[4] U[2] V[2] Y2 */
 	if (!above) {
@@ -142,66 +173,70 @@ static int read_all_tokens(TokenCtx* t, Vp8DecodedFrame* f, const uint8_t* has_y
 		return -1;
 	}
 	Vp8CoeffStats* st = t->st;
+	const int dense = sk->pk == NULL;
+	int16_t tmp[16], y2[16];
 	for (uint32_t r = 0; r < f->mb_rows; r++) {
 		uint8_t left[9] = {0};
 		for (uint32_t c = 0; c < cols; c++) {
 			const uint32_t mb = r * cols + c;
 			uint8_t* ab = above + (size_t)c * 9;
 			const int skip = f->skip_coeff[mb];
-			int any = 0;
-			int16_t* y2 = f->coeff_y2 + (size_t)mb * 16;
+			uint32_t any = 0, y2mask = 0;
+			if (!dense) sk->pk->mb_off[mb] = (uint32_t)sk->pk->n_values;
+			memset(y2, 0, sizeof(y2));
 			if (has_y2[mb]) {
 				st->blocks_total_y2++;
-				int nz = 0;
-				if (!skip) nz = read_block(t, PLANE_Y2, 0, left[8] + ab[8], y2, mb, 1, 0);
-				else memset(y2, 0, 32);
-				t->hash = hash_block(t->hash, y2);
-				st->blocks_nonzero_y2 += (uint32_t)nz;
-				any |= nz;
-				left[8] = ab[8] = (uint8_t)nz;
-			} else {
-				memset(y2, 0, 32);
+				if (!skip) y2mask = read_block(t, PLANE_Y2, 0, left[8] + ab[8], y2, mb, 1, 0);
+				if (sk->hash) t->hash = hash_block(t->hash, y2);
+				st->blocks_nonzero_y2 += y2mask != 0;
+				any |= y2mask;
+				left[8] = ab[8] = (uint8_t)(y2mask != 0);
 			}
+			if (dense) memcpy(f->coeff_y2 + (size_t)mb * 16, y2, sizeof(y2));
 			const int ytype = has_y2[mb] ? PLANE_Y_AFTER_Y2 : PLANE_Y_ALONE;
 			const int yfirst = has_y2[mb] ? 1 : 0;
 			for (int by = 0; by < 4; by++) {
 				for (int bx = 0; bx < 4; bx++) {
-					int16_t* blk = f->coeff_y + ((size_t)mb * 16 + (size_t)(by * 4 + bx)) * 16;
+					const uint32_t bi = (uint32_t)(by * 4 + bx);
+					uint32_t m = 0;
 					st->blocks_total_y++;
-					int nz = 0;
-					if (!skip) nz = read_block(t, ytype, yfirst, left[by] + ab[bx], blk, mb, 0, (uint32_t)(by * 4 + bx));
-					else memset(blk, 0, 32);
-					t->hash = hash_block(t->hash, blk);
-					st->blocks_nonzero_y += (uint32_t)nz;
-					any |= nz;
-					left[by] = ab[bx] = (uint8_t)nz;
+					if (!skip) m = read_block(t, ytype, yfirst, left[by] + ab[bx], tmp, mb, 0, bi);
+					else memset(tmp, 0, sizeof(tmp));
+					if (sk->hash) t->hash = hash_block(t->hash, tmp);
+					if (dense) memcpy(f->coeff_y + ((size_t)mb * 16 + bi) * 16, tmp, sizeof(tmp));
+					else if (sink_values(sk, mb, bi, tmp, m) != 0) goto oom;
+					st->blocks_nonzero_y += m != 0;
+					any |= m;
+					left[by] = ab[bx] = (uint8_t)(m != 0);
 				}
 			}
 			for (int pl = 0; pl < 2; pl++) { /* U then V */
-				int16_t* base = (pl == 0 ? f->coeff_u : f->coeff_v) + (size_t)mb * 64;
+				int16_t* base = (pl == 0 ? f->coeff_u : f->coeff_v);
 				uint8_t* lc = left + 4 + 2 * pl;
 				uint8_t* ac = ab + 4 + 2 * pl;
 				for (int by = 0; by < 2; by++) {
 					for (int bx = 0; bx < 2; bx++) {
-						int16_t* blk = base + (by * 2 + bx) * 16;
-						int nz = 0;
-						if (!skip)
-							nz = read_block(t, PLANE_UV, 0, lc[by] + ac[bx], blk, mb, (uint32_t)(2 + pl),
-							                (uint32_t)(by * 2 + bx));
-						else memset(blk, 0, 32);
-						t->hash = hash_block(t->hash, blk);
+						const uint32_t bi = (uint32_t)(by * 2 + bx);
+						uint32_t m = 0;
+						if (!skip) m = read_block(t, PLANE_UV, 0, lc[by] + ac[bx], tmp, mb, (uint32_t)(2 + pl), bi);
+						else memset(tmp, 0, sizeof(tmp));
+						if (sk->hash) t->hash = hash_block(t->hash, tmp);
+						if (dense) memcpy(base + ((size_t)mb * 4 + bi) * 16, tmp, sizeof(tmp));
+						else if (sink_values(sk, mb, 16u + 4u * (uint32_t)pl + bi, tmp, m) != 0) goto oom;
 						if (pl == 0) {
 							st->blocks_total_u++;
-							st->blocks_nonzero_u += (uint32_t)nz;
+							st->blocks_nonzero_u += m != 0;
 						} else {
 							st->blocks_total_v++;
-							st->blocks_nonzero_v += (uint32_t)nz;
+							st->blocks_nonzero_v += m != 0;
 						}
-						any |= nz;
-						lc[by] = ac[bx] = (uint8_t)nz;
+						any |= m;
+						lc[by] = ac[bx] = (uint8_t)(m != 0);
 					}
 				}
 			}
+			/* packed order is Y 0..15, U 0..3, V 0..3, Y2 (decode order has Y2 first) */
+			if (!dense && sink_values(sk, mb, 24, y2, y2mask) != 0) goto oom;
 			f->has_coeff[mb] = (uint8_t)(any != 0);
 		}
 	}
@@ -210,6 +245,10 @@ static int read_all_tokens(TokenCtx* t, Vp8DecodedFrame* f, const uint8_t* has_y
 	st->token_overread_bytes = vp8b_ref_overread_bytes(&t->tok);
 	st->token_overread = (uint8_t)(st->token_overread_bytes != 0);
 	return 0;
+oom:
+	free(above);
+	errno = ENOMEM;
+	return -1;
 }
 
 void vp8_decoded_frame_free(Vp8DecodedFrame* f) {
@@ -235,7 +274,7 @@ static int8_t read_opt_signed(Vp8Bool* b, int nbits) {
 	return clamp_s8(vp8b_signed(b, nbits));
 }
 
-int vp8_decode_decoded_frame(ByteSpan payload, Vp8DecodedFrame* out) {
+static int decode_frame(ByteSpan payload, Vp8DecodedFrame* out, Sink* sk) {
 	if (!out) return -1;
 	memset(out, 0, sizeof(*out));
 	Vp8KeyFrameHeader kf;
@@ -266,16 +305,28 @@ int vp8_decode_decoded_frame(ByteSpan payload, Vp8DecodedFrame* out) {
 	out->ymode = (uint8_t*)calloc(total, 1);
 	out->uv_mode = (uint8_t*)calloc(total, 1);
 	out->bmode = (uint8_t*)calloc((size_t)total * 16, 1);
-	out->coeff_y2 = (int16_t*)calloc((size_t)total * 16, sizeof(int16_t));
-	out->coeff_y = (int16_t*)calloc((size_t)total * 256, sizeof(int16_t));
-	out->coeff_u = (int16_t*)calloc((size_t)total * 64, sizeof(int16_t));
-	out->coeff_v = (int16_t*)calloc((size_t)total * 64, sizeof(int16_t));
+	int coeff_ok;
+	if (!sk->pk) {
+		out->coeff_y2 = (int16_t*)calloc((size_t)total * 16, sizeof(int16_t));
+		out->coeff_y = (int16_t*)calloc((size_t)total * 256, sizeof(int16_t));
+		out->coeff_u = (int16_t*)calloc((size_t)total * 64, sizeof(int16_t));
+		out->coeff_v = (int16_t*)calloc((size_t)total * 64, sizeof(int16_t));
+		coeff_ok = out->coeff_y2 && out->coeff_y && out->coeff_u && out->coeff_v;
+	} else {
+		/* first guess ~24 values per MB; sink_values() grows it */
+		sk->cap = (size_t)total * 24 + 1024;
+		sk->pk->masks = (uint16_t*)malloc((size_t)total * VP8G_PK_BLOCKS * sizeof(uint16_t));
+		sk->pk->mb_off = (uint32_t*)malloc((size_t)total * sizeof(uint32_t));
+		sk->pk->values = (int16_t*)malloc(sk->cap * sizeof(int16_t));
+		sk->pk->n_values = 0;
+		coeff_ok = sk->pk->masks && sk->pk->mb_off && sk->pk->values;
+	}
 	uint8_t* has_y2 = (uint8_t*)calloc(total, 1);
 	uint8_t* above_b = (uint8_t*)calloc((size_t)cols * 4, 1); /* above sub-block modes, B_DC = 0 */
 	TokenCtx* t = (TokenCtx*)calloc(1, sizeof(TokenCtx));
 	int rc = -1;
 	if (!out->segment_id || !out->skip_coeff || !out->has_coeff || !out->ymode || !out->uv_mode || !out->bmode ||
-	    !out->coeff_y2 || !out->coeff_y || !out->coeff_u || !out->coeff_v || !has_y2 || !above_b || !t) {
+	    !coeff_ok || !has_y2 || !above_b || !t) {
 		errno = ENOMEM;
 		goto done;
 	}
@@ -392,8 +443,8 @@ int vp8_decode_decoded_frame(ByteSpan payload, Vp8DecodedFrame* out) {
 	st->token_part_size_bytes = (uint32_t)(payload.size - tok_off);
 	t->st = st;
 	t->hash = 1469598103934665603ull;
-	if (read_all_tokens(t, out, has_y2) != 0) goto done;
-	st->coeff_hash_fnv1a64 = t->hash;
+	if (read_all_tokens(t, out, has_y2, sk) != 0) goto done;
+	st->coeff_hash_fnv1a64 = sk->hash ? t->hash : 0;
 	rc = 0;
 
 done:
@@ -403,7 +454,41 @@ done:
 	if (rc != 0) {
 		int e = errno;
 		vp8_decoded_frame_free(out);
+		if (sk->pk) {
+			free(sk->pk->masks);
+			free(sk->pk->mb_off);
+			free(sk->pk->values);
+			sk->pk->masks = NULL, sk->pk->mb_off = NULL, sk->pk->values = NULL, sk->pk->n_values = 0;
+		}
 		errno = e;
 	}
 	return rc;
+}
+
+int vp8_decode_decoded_frame(ByteSpan payload, Vp8DecodedFrame* out) {
+	Sink sk = {NULL, 1, 0};
+	return decode_frame(payload, out, &sk);
+}
+
+int vp8f_decode_packed(ByteSpan payload, Vp8gPackedFrame* out, unsigned flags) {
+	if (!out) {
+		errno = EINVAL;
+		return -1;
+	}
+	memset(out, 0, sizeof(*out));
+	Sink sk = {out, (flags & VP8F_PACK_HASH) != 0, 0};
+	if (vp8_parse_keyframe_header(payload, &out->kf) != 0) {
+		errno = EINVAL;
+		return -1;
+	}
+	return decode_frame(payload, &out->f, &sk);
+}
+
+void vp8f_packed_free(Vp8gPackedFrame* p) {
+	if (!p) return;
+	vp8_decoded_frame_free(&p->f);
+	free(p->masks);
+	free(p->mb_off);
+	free(p->values);
+	memset(p, 0, sizeof(*p));
 }

@@ -105,6 +105,26 @@ out:
 	return rc;
 }
 
+int vp8f_decode_packed_memory(const uint8_t* data, size_t size, Vp8gPackedFrame* out, int* stage, unsigned flags) {
+	int st = 0, rc = -1;
+	WebPContainer c;
+	ByteSpan file = {data, size};
+	if (out) memset(out, 0, sizeof(*out));
+	if (!out) {
+		errno = EINVAL;
+		st = 4;
+	} else if (webp_parse_simple_lossy(file, &c) != 0) {
+		st = 2;
+	} else {
+		ByteSpan payload = {data + c.vp8_chunk_offset, c.vp8_chunk_size};
+		if (vp8_parse_keyframe_header(payload, &out->kf) != 0 || !out->kf.is_key_frame) st = 3;
+		else if (vp8f_decode_packed(payload, out, flags) != 0) st = 4;
+		else rc = 0;
+	}
+	if (stage) *stage = st;
+	return rc;
+}
+
 int vp8f_decode_file(const char* path, Vp8KeyFrameHeader* kf, Vp8DecodedFrame* out, int* stage) {
 	FILE* fp = fopen(path, "rb");
 	if (!fp) {

@@ -111,6 +111,15 @@ class Vp8gEncDesc(C.Structure):
     ]
 
 
+class Vp8gPackedFrame(C.Structure):
+    """include/vp8g.h: packed m05 output (per block a non-zero mask, then the non-zero values)."""
+    _fields_ = [("kf", Vp8KeyFrameHeader), ("f", Vp8DecodedFrame), ("masks", C.POINTER(C.c_uint16)),
+                ("mb_off", C.POINTER(C.c_uint32)), ("values", C.POINTER(C.c_int16)), ("n_values", C.c_uint64)]
+
+
+PK_BLOCKS = 25  # per MB: Y 0..15, U 0..3, V 0..3, Y2
+VP8F_PACK_HASH = 1
+
 ENC_FORMATS = {"rgb": 0, "ppm": 1, "png": 2}
 ENC_SPAN = 32768
 
@@ -165,6 +174,10 @@ def host_lib():
         lib.vp8_decoded_frame_free.restype = None
         lib.vp8f_fnv1a64.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64]
         lib.vp8f_fnv1a64.restype = C.c_uint64
+        lib.vp8f_decode_packed_memory.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(Vp8gPackedFrame),
+                                                  C.POINTER(C.c_int), C.c_uint]
+        lib.vp8f_packed_free.argtypes = [C.POINTER(Vp8gPackedFrame)]
+        lib.vp8f_packed_free.restype = None
         lib._typed = True
     return lib
 
@@ -201,6 +214,8 @@ def gpu_lib():
         lib.vp8g_make_enc_desc.restype = C.c_uint32
         lib.vp8g_encode_batch_device.argtypes = [P(Vp8gEncDesc), C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
                                                  C.c_void_p, C.c_void_p]
+        lib.vp8g_decode_webp_batch.argtypes = [P(ByteSpan), C.c_uint32, C.c_int, C.c_uint32, P(Yuv420Image),
+                                               P(C.c_int)]
         lib._typed = True
     return lib
 
@@ -260,6 +275,77 @@ def synth_frame(width: int, height: int, seed: int, profile: int = 0) -> Frame:
     if lib.vp8f_synth_frame(width, height, seed & 0xFFFFFFFFFFFFFFFF, profile, C.byref(kf), C.byref(fr)) != 0:
         raise ValueError("synth failed")
     return Frame(kf, fr)
+
+
+class PackedFrame:
+    """Owns one Vp8gPackedFrame decoded by libvp8host (vp8f_decode_packed_memory)."""
+
+    def __init__(self, data: bytes, hash_coeffs: bool = False):
+        self.p = Vp8gPackedFrame()
+        st = C.c_int(0)
+        buf = (C.c_uint8 * len(data)).from_buffer_copy(data)
+        if host_lib().vp8f_decode_packed_memory(buf, len(data), C.byref(self.p), C.byref(st),
+                                                VP8F_PACK_HASH if hash_coeffs else 0) != 0:
+            raise ValueError(f"packed decode failed at stage {st.value}")
+        self._alive = True
+
+    def side(self, name: str) -> np.ndarray:
+        per = 16 if name == "bmode" else 1
+        return np.ctypeslib.as_array(getattr(self.p.f, name), shape=(int(self.p.f.mb_total) * per,)).copy()
+
+    def masks(self) -> np.ndarray:
+        return np.ctypeslib.as_array(self.p.masks, shape=(int(self.p.f.mb_total), PK_BLOCKS)).copy()
+
+    def mb_off(self) -> np.ndarray:
+        return np.ctypeslib.as_array(self.p.mb_off, shape=(int(self.p.f.mb_total),)).copy()
+
+    def values(self) -> np.ndarray:
+        n = int(self.p.n_values)
+        return np.ctypeslib.as_array(self.p.values, shape=(n,)).copy() if n else np.zeros(0, np.int16)
+
+    def free(self):
+        if self._alive:
+            host_lib().vp8f_packed_free(C.byref(self.p))
+            self._alive = False
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def unpack_coeffs(pf: PackedFrame) -> dict:
+    """Host restatement of the device expansion (expand_kernel): packed -> the four dense arrays
+    (test infrastructure)."""
+    masks, off, vals = pf.masks().astype(np.uint32), pf.mb_off().astype(np.int64), pf.values()
+    nmb = masks.shape[0]
+    dense = np.zeros((nmb, PK_BLOCKS, 16), np.int16)
+    bits = ((masks[:, :, None] >> np.arange(16, dtype=np.uint32)) & 1).astype(bool)  # [mb, block, pos]
+    flat = bits.reshape(nmb, -1)
+    rank = np.cumsum(flat, axis=1) - 1  # index of each non-zero among the MB's values
+    src = off[:, None] + rank
+    dense.reshape(nmb, -1)[flat] = vals[src[flat]]
+    return {"coeff_y": dense[:, :16].reshape(-1), "coeff_u": dense[:, 16:20].reshape(-1),
+            "coeff_v": dense[:, 20:24].reshape(-1), "coeff_y2": dense[:, 24].reshape(-1)}
+
+
+def gpu_decode_webp_batch(files: list[bytes], filtered: bool = True, threads: int = 0):
+    """vp8g_decode_webp_batch: .webp images -> (list of I420 bytes or None, list of errno)."""
+    lib = gpu_lib()
+    n = len(files)
+    bufs = [(C.c_uint8 * max(1, len(b))).from_buffer_copy(b if b else b"\0") for b in files]
+    spans = (ByteSpan * n)(*[ByteSpan(C.cast(bufs[i], C.POINTER(C.c_uint8)), len(files[i])) for i in range(n)])
+    imgs = (Yuv420Image * n)()
+    st = (C.c_int * n)()
+    rc = lib.vp8g_decode_webp_batch(spans, n, int(filtered), threads, imgs, st)
+    if rc != 0 and all(s == 5 for s in st):  # EIO: device failure, nothing returned
+        raise RuntimeError(f"vp8g_decode_webp_batch failed: {lib.vp8g_last_error()!r}")
+    out = []
+    for i in range(n):
+        out.append(_image_bytes(imgs[i]) if st[i] == 0 else None)
+        lib.yuv420_free(C.byref(imgs[i]))
+    return out, list(st)
 
 
 def fnv1a64(buf: bytes | np.ndarray, h: int = 1469598103934665603) -> int:
