@@ -65,7 +65,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
-    ap.add_argument("--e2e-frames", type=int, default=96,
+    ap.add_argument("--e2e-frames", type=int, default=256,
                     help="frames of the end-to-end object (.webp bytes -> I420, vp8g_decode_webp_batch); 0 = off")
     ap.add_argument("--encode", default="png", choices=["none", "rgb", "ppm", "png"],
                     help="also time the m08/m09 stage on the batch's output (secondary object 'encode')")
@@ -176,7 +176,7 @@ def end_to_end(manifest, n_frames, filtered, threads):
         import subprocess
         import tempfile
         from concurrent.futures import ThreadPoolExecutor
-        n_ref = 2 * threads
+        n_ref = 8 * threads
         with tempfile.TemporaryDirectory() as td:
             src = [pathlib.Path(td) / f"f{i}.webp" for i in range(4)]
             for i in range(4):

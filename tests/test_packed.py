@@ -66,3 +66,45 @@ def test_packed_errors(vp8g, name, stage):
     assert vp8g.host_lib().vp8f_decode_packed_memory(buf, len(data), C.byref(p), C.byref(st), 0) == -1
     assert st.value >= stage
     assert not p.masks and not p.values and not p.f.ymode  # nothing leaked / left allocated
+
+
+def truncated_payload(data: bytes, frac: float) -> bytes:
+    """The same .webp with its VP8 payload cut to `frac` (container sizes rewritten), so the token
+    partition runs past its end and the bool decoder's overread diagnostics come into play."""
+    import struct
+    csize = struct.unpack("<I", data[16:20])[0]
+    c = int(csize * frac)
+    c -= c & 1
+    return b"RIFF" + struct.pack("<I", 12 + c) + b"WEBPVP8 " + struct.pack("<I", c) + data[20:20 + c]
+
+
+@pytest.mark.skipif(not (ROOT / "oracle" / "_ref" / "libref.so").exists(), reason="reference not built here")
+def test_front_end_stats_equal_reference_on_truncated_streams(vp8g, manifest, tmp_path):
+    """m05 statistics (Vp8CoeffStats: counts, hash, bytes used, first overread position and stage,
+    vp8_tokens.c:970-998 and bool_decoder.c:5-39) of the host front end -- dense and packed -- equal the
+    reference's own m05 (oracle/_ref/libref.so) on intact and truncated payloads."""
+    import ctypes as C
+    ref = vp8g.ref_lib()
+    host = vp8g.host_lib()
+    n_ovr = 0
+    for rel in sorted(manifest["files"])[::9]:
+        data = (FIXTURES / rel).read_bytes()
+        for frac in (1.0, 0.95, 0.8):
+            case = data if frac == 1.0 else truncated_payload(data, frac)
+            path = tmp_path / "case.webp"
+            path.write_bytes(case)
+            kf, rf = vp8g.Vp8KeyFrameHeader(), vp8g.Vp8DecodedFrame()
+            rrc = ref.ref_decode_frame(str(path).encode(), C.byref(kf), C.byref(rf))
+            kf2, df, st = vp8g.Vp8KeyFrameHeader(), vp8g.Vp8DecodedFrame(), C.c_int(0)
+            buf = (C.c_uint8 * len(case)).from_buffer_copy(case)
+            drc = host.vp8f_decode_memory(buf, len(case), C.byref(kf2), C.byref(df), C.byref(st))
+            assert (rrc == 0) == (drc == 0), (rel, frac)
+            if rrc == 0:
+                assert bytes(df.stats) == bytes(rf.stats), (rel, frac)
+                n_ovr += rf.stats.token_overread
+                pf = vp8g.PackedFrame(case, hash_coeffs=True)
+                assert bytes(pf.p.f.stats) == bytes(rf.stats), (rel, frac, "packed")
+                pf.free()
+                ref.ref_free_frame(C.byref(rf))
+                host.vp8_decoded_frame_free(C.byref(df))
+    assert n_ovr > 10  # the truncations did reach the overread paths

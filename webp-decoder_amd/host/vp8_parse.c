@@ -28,11 +28,8 @@
 enum { TOK_ZERO = 0, TOK_ONE, TOK_TWO, TOK_THREE, TOK_FOUR, TOK_CAT1, TOK_CAT2, TOK_CAT3, TOK_CAT4,
        TOK_CAT5, TOK_CAT6, TOK_EOB };
 
-/* RFC 6386 13.2 token tree */
-static const int8_t k_token_tree[22] = {
-    -TOK_EOB, 2, -TOK_ZERO, 4, -TOK_ONE, 6, 8, 12, -TOK_TWO, 10, -TOK_THREE, -TOK_FOUR,
-    14, 16, -TOK_CAT1, -TOK_CAT2, 18, 20, -TOK_CAT3, -TOK_CAT4, -TOK_CAT5, -TOK_CAT6,
-};
+/* RFC 6386 13.2 token tree {-EOB, 2, -ZERO, 4, -ONE, 6, 8, 12, -TWO, 10, -THREE, -FOUR, 14, 16,
+ * -CAT1, -CAT2, 18, 20, -CAT3, -CAT4, -CAT5, -CAT6}: walked as straight code in read_block */
 /* RFC 6386 13.3 band of each scan position, and zigzag scan -> natural index */
 static const uint8_t k_band[17] = {0, 1, 2, 3, 6, 4, 5, 6, 6, 6, 6, 6, 6, 6, 6, 7, 0};
 static const uint8_t k_scan[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
@@ -82,9 +79,10 @@ typedef struct {
 	Vp8Bool tok;                /* token partition */
 	Vp8CoeffStats* st;
 	uint64_t hash;
+	uint64_t ovr_shift; /* shift count at which the reference-equivalent overread becomes non-zero */
 } TokenCtx;
 
-static void note_overread(TokenCtx* t, uint32_t mb, uint32_t plane, uint32_t blk, uint32_t pos, uint32_t stage) {
+static void note_overread_slow(TokenCtx* t, uint32_t mb, uint32_t plane, uint32_t blk, uint32_t pos, uint32_t stage) {
 	Vp8CoeffStats* st = t->st;
 	if (st->token_overread_mb_index != 0xFFFFFFFFu) return;
 	if (vp8b_ref_overread_bytes(&t->tok) == 0) return;
@@ -94,42 +92,80 @@ static void note_overread(TokenCtx* t, uint32_t mb, uint32_t plane, uint32_t blk
 	st->token_overread_coeff_i = pos;
 	st->token_overread_stage = stage;
 }
+/* first position at which the partition was over-read (reference diagnostics, `decoder -info`) */
+#define NOTE_OVERREAD(t, mb, plane, blk, pos, stage) \
+	do { \
+		if ((t)->tok.shifts >= (t)->ovr_shift) note_overread_slow(t, mb, plane, blk, pos, stage); \
+	} while (0)
+
+/* DCT_CAT1..6 magnitude: base + extra bits (RFC 6386 13.2) */
+static inline int read_cat(Vp8Bool* b, int cat) {
+	const uint8_t* ep = k_cat_probs[cat];
+	int extra = 0;
+	for (; *ep; ep++) extra = (extra << 1) | vp8b_read(b, *ep);
+	return k_cat_base[cat] + extra;
+}
 
 /* Decodes one 4x4 block's tokens (RFC 6386 13) into out[] (natural order).  Returns the mask of
  * natural positions holding a non-zero value (the block "has coefficients" iff it is non-zero).
- * `plane_tag` is only for the overread diagnostics (0=Y 1=Y2 2=U 3=V). */
+ * The token tree (13.2) is walked as straight code: node 0 (p[0]) EOB?, node 2
+ * (p[1]) ZERO?, node 4 (p[2]) ONE?, then TWO/THREE/FOUR (p[3..5]) or the categories (p[6..10]);
+ * after a ZERO the next token starts at node 2 (no EOB).  `plane_tag` is only for the overread
+ * diagnostics (0=Y 1=Y2 2=U 3=V). */
 static uint32_t read_block(TokenCtx* t, int type, int first, int ctx, int16_t out[16], uint32_t mb, uint32_t plane_tag,
                            uint32_t blk) {
 	Vp8CoeffStats* st = t->st;
+	Vp8Bool* b = &t->tok;
+	uint8_t(*P)[3][11] = t->probs[type];
 	memset(out, 0, 16 * sizeof(int16_t));
 	uint32_t mask = 0;
-	int after_zero = 0;
-	for (int pos = first; pos < 16; pos++) {
-		const uint8_t* p = t->probs[type][k_band[pos]][ctx];
-		int tok = vp8b_tree(&t->tok, k_token_tree, p, after_zero ? 2 : 0);
-		note_overread(t, mb, plane_tag, blk, (uint32_t)pos, 0);
-		if (tok == TOK_EOB) {
-			st->coeff_eob_tokens++;
-			break;
+	int pos = first;
+	const uint8_t* p = P[k_band[pos]][ctx];
+	int skip_eob = 0;
+	while (pos < 16) {
+		if (!skip_eob) {
+			const int more = vp8b_read(b, p[0]);
+			if (!more) {
+				NOTE_OVERREAD(t, mb, plane_tag, blk, (uint32_t)pos, 0);
+				st->coeff_eob_tokens++;
+				break;
+			}
 		}
-		int mag = tok; /* ZERO..FOUR are their own magnitude */
-		if (tok >= TOK_CAT1) {
-			const uint8_t* ep = k_cat_probs[tok - TOK_CAT1];
-			int extra = 0;
-			for (; *ep; ep++) extra = (extra << 1) | vp8b_read(&t->tok, *ep);
-			note_overread(t, mb, plane_tag, blk, (uint32_t)pos, 1);
-			mag = k_cat_base[tok - TOK_CAT1] + extra;
+		if (!vp8b_read(b, p[1])) { /* DCT_0 */
+			NOTE_OVERREAD(t, mb, plane_tag, blk, (uint32_t)pos, 0);
+			if (++pos == 16) break;
+			p = P[k_band[pos]][0];
+			skip_eob = 1;
+			continue;
 		}
-		if (mag) {
-			int neg = vp8b_read(&t->tok, 128);
-			note_overread(t, mb, plane_tag, blk, (uint32_t)pos, 2);
-			out[k_scan[pos]] = (int16_t)(neg ? -mag : mag);
-			mask |= 1u << k_scan[pos];
-			st->coeff_nonzero_total++;
-			if ((uint32_t)mag > st->coeff_abs_max) st->coeff_abs_max = (uint32_t)mag;
+		int mag;
+		if (!vp8b_read(b, p[2])) {
+			mag = 1;
+			NOTE_OVERREAD(t, mb, plane_tag, blk, (uint32_t)pos, 0);
+		} else {
+			if (!vp8b_read(b, p[3])) {
+				if (!vp8b_read(b, p[4])) mag = 2;
+				else mag = 3 + vp8b_read(b, p[5]);
+				NOTE_OVERREAD(t, mb, plane_tag, blk, (uint32_t)pos, 0);
+			} else {
+				int cat;
+				if (!vp8b_read(b, p[6])) cat = vp8b_read(b, p[7]);
+				else if (!vp8b_read(b, p[8])) cat = 2 + vp8b_read(b, p[9]);
+				else cat = 4 + vp8b_read(b, p[10]);
+				NOTE_OVERREAD(t, mb, plane_tag, blk, (uint32_t)pos, 0);
+				mag = read_cat(b, cat);
+				NOTE_OVERREAD(t, mb, plane_tag, blk, (uint32_t)pos, 1);
+			}
 		}
-		ctx = mag == 0 ? 0 : (mag == 1 ? 1 : 2);
-		after_zero = (tok == TOK_ZERO);
+		const int neg = vp8b_read(b, 128);
+		NOTE_OVERREAD(t, mb, plane_tag, blk, (uint32_t)pos, 2);
+		out[k_scan[pos]] = (int16_t)(neg ? -mag : mag);
+		mask |= 1u << k_scan[pos];
+		st->coeff_nonzero_total++;
+		if ((uint32_t)mag > st->coeff_abs_max) st->coeff_abs_max = (uint32_t)mag;
+		if (++pos == 16) break;
+		p = P[k_band[pos]][mag == 1 ? 1 : 2];
+		skip_eob = 0;
 	}
 	return mask;
 }
@@ -443,6 +479,8 @@ static int decode_frame(ByteSpan payload, Vp8DecodedFrame* out, Sink* sk) {
 	st->token_part_size_bytes = (uint32_t)(payload.size - tok_off);
 	t->st = st;
 	t->hash = 1469598103934665603ull;
+	/* overread iff (shifts >> 3) > size - min(size, 2)  (vp8b_ref_overread_bytes) */
+	t->ovr_shift = ((uint64_t)(t->tok.size - vp8b_ref_init_bytes(&t->tok)) + 1u) * 8u;
 	if (read_all_tokens(t, out, has_y2, sk) != 0) goto done;
 	st->coeff_hash_fnv1a64 = sk->hash ? t->hash : 0;
 	rc = 0;
