@@ -1,18 +1,21 @@
 // vp8g_rgb.hip -- m08 / m09 on the GPU: "fancy" 4:2:0 upsampled I420 -> RGB24 and the exact
 // PPM / PNG files the reference writes (src/m08_yuv2rgb_ppm/yuv2rgb_ppm.c, src/m09_png/yuv2rgb_png.c).
 //
-// The output FILE is the unit of work: it is cut into VP8G_ENC_SPAN-byte spans, one workgroup
-// task each (a workgroup loops over tasks).  A task
-//   1. computes the pixel bytes that land in its span (one thread per horizontal pixel pair: the
-//      pair shares its four chroma samples and the 9:3:3:1 diagonals) and the few layout bytes
-//      (PPM header; PNG signature / IHDR / IDAT header / zlib header, the 5-byte stored-block
-//      headers, the IEND trailer) into an LDS image of the span;
-//   2. streams the span to HBM as 16-byte stores, 64 contiguous bytes per thread, and -- PNG --
-//      folds the same bytes into a CRC-32 (slice-by-8 tables) and Adler-32 partial sums;
-//   3. combines the 512 thread CRCs with GF(2) shift operators (nibble tables in LDS) into one
-//      CRC per span, written with the span's Adler partials to the workspace.
-// A second, small launch (one workgroup per PNG) combines the span partials and writes the
-// Adler-32 and the IDAT CRC.  Every byte of every file is produced on the device.
+// The output FILE is the unit of work: it is cut into VP8G_ENC_SPAN-byte spans (32 KB), one
+// workgroup task each (a workgroup loops over tasks).
+//   enc_write_kernel (every format) writes a span's bytes straight to HBM: one thread per 12-pixel
+//     chunk of a row (six pixel pairs, each pair sharing four chroma samples and the 9:3:3:1
+//     diagonals; one unaligned 8-byte load per chroma row and plane with the edge columns
+//     replicated, one 12-byte luma load; 36 bytes out with unaligned 8-byte stores), plus the few
+//     layout bytes (PPM header; PNG signature / IHDR / IDAT header / zlib header, the 5-byte
+//     stored-block headers, the IEND trailer).  No LDS and no barriers: the waves of a CU overlap
+//     their memory latency freely.
+//   crc_kernel (PNG) re-reads each span, 32 contiguous bytes per thread, folds them into a CRC-32
+//     (slice-by-8 tables in LDS) and Adler-32 partial sums, and combines the 1024 thread partials
+//     (lane shuffles inside a wave, GF(2) shift operators as nibble tables) into one per span.
+//   png_finish_kernel (one workgroup per PNG) combines the span partials with host-precomputed
+//     operators and writes the Adler-32 and the IDAT CRC.
+// Every byte of every file is produced on the device.
 //
 // CRC algebra (reflected CRC-32, polynomial 0xEDB88320): the raw register update is linear, so
 // with Z_n = "feed n zero bytes", crc_raw(A || B) = Z_|B|(crc_raw(A)) ^ crc_raw(B), leading zero
@@ -43,7 +46,8 @@ constexpr int kThreads = 1024;                     // task kernel
 constexpr uint32_t kPerThread = kSpan / kThreads;  // 32 contiguous file bytes per thread
 constexpr int kFinThreads = 256;                   // PNG finishing kernel
 constexpr int kFinLevels = 8;                      // log2(kFinThreads)
-constexpr uint32_t kGroup = 4;                     // pixel-pair units per thread and iteration
+constexpr uint32_t kChunk = 12;                     // pixels of a row per thread and iteration (36 bytes)
+constexpr uint32_t kUnits = kChunk / 2;            // pixel-pair units m .. m + kUnits touched by a chunk
 constexpr uint32_t kMod = 65521u;                  // Adler-32
 constexpr uint32_t kBlk = 65535u;                  // stored-deflate block payload
 constexpr uint32_t kBlkFile = kBlk + 5u;           // ... plus its header
@@ -53,17 +57,19 @@ constexpr uint32_t kCrcStart = 37u;                // IDAT CRC covers the chunk 
 constexpr int kTreeLevels = 10;                    // log2(kThreads)
 static_assert(kSpan % kThreads == 0 && kPerThread % 16 == 0, "span layout");
 
-// Tables shared by every task (12.5 KB): CRC-32 slice-by-8 tables T0..T7, then for the in-span
-// tree the nibble tables of Z_{64 * 2^l}, l = 0..8: tab[2048 + 128 l + 16 j + v] = Z(v << 4j).
+// Tables shared by every task (13 KB): CRC-32 slice-by-8 tables T0..T7, then for the in-span
+// tree the nibble tables of Z_{32 * 2^l}, l = 0..9: tab[2048 + 128 l + 16 j + v] = Z(v << 4j).
 constexpr int kSlice = 8;
 constexpr int kNibBase = kSlice * 256;
 constexpr int kTabWords = kNibBase + kTreeLevels * 8 * 16;
 
-struct EncLds {
-	uint8_t buf[kSpan];
+struct CrcLds {
 	uint32_t tab[kTabWords];
-	uint32_t red[3][kThreads];
+	uint32_t red[2][3][kThreads / 64];  // per-wave partials, double-buffered by task parity
 };
+
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
 
 // ---- device helpers ----------------------------------------------------------------------
 // reference yuv2rgb_ppm.c:19-42: libwebp VP8YuvToRgb (14-bit fixed point, clip of v >> 6)
@@ -79,6 +85,19 @@ DEV uint32_t yuv_rgb(int y, int u, int v) {  // packed r | g << 8 | b << 16
 	return r | (g << 8) | (b << 16);
 }
 
+// One unit = pixels {2k-1, 2k} of a row (reference yuv2rgb_ppm.c:44-121): it blends chroma columns
+// k-1 and k of the two chroma rows around the pixel row (at the edges both columns are one, which
+// gives the 3:1 edge formula exactly).  (tl, t) = row a, (l, u) = row b; near_a = the pixel row is
+// nearer row a.  Returns the two pixels' colours.
+DEV void pair_rgb(bool near_a, int tlu, int tu, int lu, int uu, int tlv, int tv, int lv, int uv, int y_odd, int y_even,
+                  uint32_t& c_odd, uint32_t& c_even) {
+	const int au = tlu + tu + lu + uu + 8, av = tlv + tv + lv + uv + 8;
+	const int d12u = (au + 2 * (tu + lu)) >> 3, d03u = (au + 2 * (tlu + uu)) >> 3;
+	const int d12v = (av + 2 * (tv + lv)) >> 3, d03v = (av + 2 * (tlv + uv)) >> 3;
+	c_odd = yuv_rgb(y_odd, near_a ? (d12u + tlu) >> 1 : (d03u + lu) >> 1, near_a ? (d12v + tlv) >> 1 : (d03v + lv) >> 1);
+	c_even = yuv_rgb(y_even, near_a ? (d03u + tu) >> 1 : (d12u + uu) >> 1, near_a ? (d03v + tv) >> 1 : (d12v + uv) >> 1);
+}
+
 // file offset of pixel-stream byte p (PNG: stored blocks of kBlk bytes behind 5-byte headers)
 DEV uint32_t png_file_of_raw(uint32_t p) { return kPngRaw0 + p + 5u * (p / kBlk); }
 // first pixel-stream byte at or after file offset q, clamped to n
@@ -89,6 +108,8 @@ DEV uint32_t raw_of_file(const Vp8gEncDesc& d, uint32_t q) {
 	return min(k * kBlk + (o < 5u ? 0u : o - 5u), d.raw_len);
 }
 
+DEV uint32_t byte_of2(u32x2 v, int i) { return ((i < 4 ? v.x : v.y) >> (8 * (i & 3))) & 255u; }
+DEV uint32_t byte_of3(u32x3 v, int i) { return ((i < 4 ? v.x : (i < 8 ? v.y : v.z)) >> (8 * (i & 3))) & 255u; }
 DEV uint32_t crc_byte(const uint32_t* t0, uint32_t c, uint32_t b) { return t0[(c ^ b) & 255u] ^ (c >> 8); }
 DEV uint32_t crc_dword2(const uint32_t* t, uint32_t c, uint32_t w0, uint32_t w1) {  // slice-by-8, 8 bytes
 	c ^= w0;
@@ -101,6 +122,10 @@ DEV uint32_t nib_apply(const uint32_t* nt, uint32_t v) {  // GF(2) operator via 
 	for (int j = 0; j < 8; j++) r ^= nt[j * 16 + ((v >> (4 * j)) & 15u)];
 	return r;
 }
+DEV uint32_t mod_add(uint32_t a, uint32_t b) {  // (a + b) mod 65521 for a, b < 65521
+	const uint32_t t = a + b;
+	return t >= kMod ? t - kMod : t;
+}
 DEV uint32_t op_apply(const uint32_t* col, uint32_t v) {  // GF(2) operator by columns
 	uint32_t r = 0;
 #pragma unroll
@@ -108,159 +133,148 @@ DEV uint32_t op_apply(const uint32_t* col, uint32_t v) {  // GF(2) operator by c
 	return r;
 }
 
-// ---- task kernel -------------------------------------------------------------------------
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void enc_kernel(const Vp8gEncDesc* __restrict__ D, uint32_t n, uint32_t total,
-                                                       const uint8_t* __restrict__ src, uint8_t* __restrict__ out,
-                                                       uint32_t* __restrict__ part, const uint32_t* __restrict__ tables) {
-	__shared__ EncLds L;
+// 8 chroma samples, columns m1 .. m1 + 7 of one row (m1 >= -1), with the edge rule of the
+// upsampler (reference yuv2rgb_ppm.c:44-121: column -1 reads column 0, columns >= cw read cw - 1):
+// one unaligned 8-byte load inside the row, then the missing edge bytes replicated.  cw >= 8.
+DEV uint64_t chroma8(const uint8_t* row, int m1, int cw) {
+	const int s = min(max(m1, 0), cw - 8);
+	uint64_t v = *(const uint64_t*)(row + s);  // unaligned: gfx950 runs in unaligned mode (tools/ubench/unaligned.hip)
+	const int dl = m1 - s;                     // -1 (left edge), 0 (inside), 1..7 (right edge)
+	if (dl < 0) v = (v << 8) | (v & 0xFFu);
+	if (dl > 0) v = (v >> (8 * dl)) | (((v >> 56) * 0x0101010101010101ull) << (64 - 8 * dl));
+	return v;
+}
+DEV uint32_t byte8(uint64_t v, int i) { return (uint32_t)(v >> (8 * i)) & 255u; }
+
+// Pixel bytes of the span [F0, F0 + kSpan) of image d's file, written straight into the file:
+// thread tid of NT takes chunks of kChunk pixels of a row (chunk index = row * chunks per row +
+// column chunk) and stores its 36 bytes with unaligned 8-byte stores (full lines form in L2 from
+// the neighbouring threads).  A chunk that straddles two spans is written whole by both, with
+// the same bytes.  (Assembling each wave's run in LDS for aligned 16-byte stores was measured
+// slower: the extra registers cost more occupancy than the coalescing gained.)
+template <int NT>
+DEV void span_pixels(const Vp8gEncDesc& d, bool png, uint32_t F0, uint32_t tid, const uint8_t* __restrict__ src,
+                     uint8_t* __restrict__ file) {
+	const uint32_t p_lo = raw_of_file(d, F0), p_hi = raw_of_file(d, F0 + kSpan);
+	if (p_lo >= p_hi) return;
+	const uint32_t W = d.width, SB = d.row_bytes, f = png ? 1u : 0u;
+	const uint32_t cw = (W + 1u) >> 1, ch = (d.height + 1u) >> 1;
+	const uint32_t CPR = (W + kChunk - 1u) / kChunk;  // chunks per row
+	const uint32_t ylo = p_lo / SB, rlo = p_lo - ylo * SB, xlo = rlo < f ? 0u : (rlo - f) / 3u;
+	const uint32_t yhi = (p_hi - 1u) / SB, rhi = p_hi - 1u - yhi * SB, xhi = rhi < f ? 0u : (rhi - f) / 3u;
+	const uint32_t g_first = ylo * CPR + xlo / kChunk, g_last = yhi * CPR + xhi / kChunk;
+	const uint8_t* Y = src + d.src_y;
+	const uint8_t* U = src + d.src_u;
+	const uint8_t* V = src + d.src_v;
+	auto file_of = [&](uint32_t pi) { return png ? kPngRaw0 + pi + 5u * (pi / kBlk) : d.prefix_len + pi; };
+	for (uint32_t gc = g_first + tid; gc <= g_last; gc += NT) {
+		const uint32_t y = gc / CPR, x0 = (gc - y * CPR) * kChunk, m = x0 >> 1;
+		// chroma rows (reference yuv2rgb_ppm.c:178-202): row 0 uses row 0 twice; row y sits between
+		// a = (y-1)/2 and b = min(a+1, ch-1), nearer a when y is odd
+		const uint32_t a = y ? (y - 1u) >> 1 : 0u, b = y ? min(a + 1u, ch - 1u) : 0u;
+		const bool near_a = y == 0 || (y & 1u);
+		const uint32_t rowp = y * SB;
+		if (png && x0 == 0) file[file_of(rowp)] = 0;  // the scanline's filter byte (0 = none)
+		const uint32_t p0 = rowp + f + 3u * x0;          // raw offset of the chunk's first pixel byte
+		if (x0 + kChunk <= W && cw >= 8u) {
+			// units m .. m+6 (unit k = pixels 2k-1, 2k) over chroma columns m-1 .. m+6 of rows a, b;
+			// pixel x0 + 2i is the even pixel of unit m+i, x0 + 2i - 1 the odd pixel of unit m+i
+			const int m1 = (int)m - 1;
+			const uint64_t ua = chroma8(U + a * d.stride_uv, m1, (int)cw), ub = chroma8(U + b * d.stride_uv, m1, (int)cw);
+			const uint64_t va = chroma8(V + a * d.stride_uv, m1, (int)cw), vb = chroma8(V + b * d.stride_uv, m1, (int)cw);
+			const u32x3 yl = *(const u32x3*)(Y + y * d.stride_y + x0);
+			uint32_t c[kChunk];
+#pragma unroll
+			for (int i = 0; i <= (int)kUnits; i++) {
+				uint32_t c_odd, c_even;
+				const int yo = i ? (int)byte_of3(yl, 2 * i - 1) : 0, ye = i < (int)kUnits ? (int)byte_of3(yl, 2 * i) : 0;
+				pair_rgb(near_a, (int)byte8(ua, i), (int)byte8(ua, i + 1), (int)byte8(ub, i), (int)byte8(ub, i + 1),
+				         (int)byte8(va, i), (int)byte8(va, i + 1), (int)byte8(vb, i), (int)byte8(vb, i + 1), yo, ye, c_odd, c_even);
+				if (i) c[2 * i - 1] = c_odd;
+				if (i < (int)kUnits) c[2 * i] = c_even;
+			}
+			// 12 pixels -> 36 bytes -> 9 dwords (4 pixels = 3 dwords)
+			uint32_t w[9];
+#pragma unroll
+			for (int k = 0; k < 3; k++) {
+				w[3 * k + 0] = c[4 * k] | (c[4 * k + 1] << 24);
+				w[3 * k + 1] = (c[4 * k + 1] >> 8) | (c[4 * k + 2] << 16);
+				w[3 * k + 2] = (c[4 * k + 2] >> 16) | (c[4 * k + 3] << 8);
+			}
+			if (!png || p0 / kBlk == (p0 + 3u * kChunk - 1u) / kBlk) {
+				// unaligned 8-byte stores (gfx950 runs in unaligned mode, tools/ubench/unaligned.hip)
+				uint8_t* o = file + file_of(p0);
+#pragma unroll
+				for (int k = 0; k < 4; k++) *(u32x2*)(o + 8 * k) = u32x2{w[2 * k], w[2 * k + 1]};
+				*(uint32_t*)(o + 32) = w[8];
+			} else {  // a stored-block header falls inside the chunk: byte by byte
+#pragma unroll
+				for (uint32_t i = 0; i < 3u * kChunk; i++) file[file_of(p0 + i)] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+			}
+			continue;
+		}
+		// generic chunk (a row's last, partial chunk; images narrower than 15 pixels): pixel by pixel
+		const uint32_t xe = min(x0 + kChunk, W);
+		for (uint32_t x = x0; x < xe; x++) {
+			const uint32_t k = (x + 1u) >> 1;  // unit: pixels 2k-1 (odd x) and 2k (even x)
+			const uint32_t cl = k ? k - 1u : 0u, cr = min(k, cw - 1u);
+			const uint32_t ra = a * d.stride_uv, rb = b * d.stride_uv;
+			uint32_t c_odd, c_even;
+			const int yv = Y[y * d.stride_y + x];
+			pair_rgb(near_a, U[ra + cl], U[ra + cr], U[rb + cl], U[rb + cr], V[ra + cl], V[ra + cr], V[rb + cl], V[rb + cr], yv, yv,
+			         c_odd, c_even);
+			const uint32_t col = (x & 1u) ? c_odd : c_even;
+			const uint32_t pb = rowp + f + 3u * x;
+#pragma unroll
+			for (uint32_t i = 0; i < 3; i++) file[file_of(pb + i)] = (uint8_t)(col >> (8 * i));
+		}
+	}
+}
+
+// ---- PNG checksum kernel: one workgroup task per 32 KB span of a PNG file already written by
+// enc_write_kernel; 32 contiguous bytes per thread folded into a CRC-32 (slice-by-8 tables in LDS)
+// and Adler-32 partial sums, then combined over the span (below).
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void crc_kernel(
+    const Vp8gEncDesc* __restrict__ D, uint32_t n, uint32_t total, const uint8_t* __restrict__ out,
+    uint32_t* __restrict__ part, const uint32_t* __restrict__ tables) {
+	__shared__ CrcLds L;
 	const uint32_t tid = threadIdx.x;
 	for (uint32_t i = tid; i < (uint32_t)kTabWords; i += kThreads) L.tab[i] = tables[i];
-	uint32_t img = 0;
+	__syncthreads();
+	// The next task's 32 bytes per thread are loaded before the current task is folded and reduced,
+	// so the HBM latency of a task overlaps the previous task's work.
+	auto fetch = [&](uint32_t g, uint32_t& im, uint32_t* v) {
+		while (im + 1 < n && D[im + 1].span0 <= g) im++;  // tasks are numbered image by image
+		const Vp8gEncDesc& dd = D[im];
+		const uint32_t q = (g - dd.span0) * kSpan + tid * kPerThread, fl = (uint32_t)dd.file_len;
+		const bool use = dd.format == VP8G_ENC_PNG;
+#pragma unroll
+		for (uint32_t i = 0; i < kPerThread / 16u; i++) {
+			const uint4 x = use && q + 16u * i < fl ? *(const uint4*)(out + dd.out + q + 16u * i) : make_uint4(0, 0, 0, 0);
+			v[4 * i] = x.x, v[4 * i + 1] = x.y, v[4 * i + 2] = x.z, v[4 * i + 3] = x.w;
+		}
+	};
+	uint32_t img = 0, img_next = 0, tcount = 0;
+	uint32_t nxt[kPerThread / 4u];
+	if (blockIdx.x < total) fetch(blockIdx.x, img_next, nxt);
 	for (uint32_t g = blockIdx.x; g < total; g += gridDim.x) {
-		while (img + 1 < n && D[img + 1].span0 <= g) img++;  // tasks are numbered image by image
+		img = img_next;
+		uint32_t bw[kPerThread / 4u];
+#pragma unroll
+		for (uint32_t i = 0; i < kPerThread / 4u; i++) bw[i] = nxt[i];
+		if (g + gridDim.x < total) fetch(g + gridDim.x, img_next, nxt);
 		const Vp8gEncDesc& d = D[img];
-		const bool png = d.format == VP8G_ENC_PNG;
+		if (d.format != VP8G_ENC_PNG) continue;
 		const uint32_t F0 = (g - d.span0) * kSpan;  // file offset of this span
-		const uint32_t flen = (uint32_t)d.file_len;
-		__syncthreads();  // the previous task's LDS readers are done (and the tables are loaded)
-
-		// -- 1a. pixel bytes of the span: one thread per unit k of a row = pixels {2k-1, 2k}
-		const uint32_t p_lo = raw_of_file(d, F0), p_hi = raw_of_file(d, F0 + kSpan);
-		if (p_lo < p_hi) {
-			const uint32_t W = d.width, H = d.height, SB = d.row_bytes, f = png ? 1u : 0u;
-			const uint32_t UPR = W / 2u + 1u, cw = (W + 1u) >> 1, ch = (H + 1u) >> 1;
-			const uint32_t ylo = p_lo / SB, rlo = p_lo - ylo * SB, xlo = rlo < f ? 0u : (rlo - f) / 3u;
-			const uint32_t yhi = (p_hi - 1u) / SB, rhi = p_hi - 1u - yhi * SB, xhi = rhi < f ? 0u : (rhi - f) / 3u;
-			const uint32_t gu0 = ylo * UPR + ((xlo + 1u) >> 1), gu1 = yhi * UPR + ((xhi + 1u) >> 1) + 1u;
-			const float inv = 1.0f / (float)UPR;
-			const uint8_t* Y = src + d.src_y;
-			const uint8_t* U = src + d.src_u;
-			const uint8_t* V = src + d.src_v;
-			// One unit = pixels {2k-1, 2k} of row y.  Chroma rows (reference yuv2rgb_ppm.c:178-202):
-			// row 0 uses row 0 twice; row y sits between a = (y-1)/2 and b = min(a+1, ch-1), nearer a
-			// when y is odd.  Columns (yuv2rgb_ppm.c:44-121): the pair blends columns k-1 and k; at the
-			// edges both are one column, which gives the 3:1 edge formula exactly.  Each returns the
-			// two pixels' colours (r | g << 8 | b << 16) from the 2x2 chroma samples (tl, t, l, u).
-			auto pair_rgb = [](bool near_a, int tlu, int tu, int lu, int uu, int tlv, int tv, int lv, int uv, int y_odd,
-			                   int y_even, uint32_t& c_odd, uint32_t& c_even) {
-				const int au = tlu + tu + lu + uu + 8, av = tlv + tv + lv + uv + 8;
-				const int d12u = (au + 2 * (tu + lu)) >> 3, d03u = (au + 2 * (tlu + uu)) >> 3;
-				const int d12v = (av + 2 * (tv + lv)) >> 3, d03v = (av + 2 * (tlv + uv)) >> 3;
-				c_odd = yuv_rgb(y_odd, near_a ? (d12u + tlu) >> 1 : (d03u + lu) >> 1, near_a ? (d12v + tlv) >> 1 : (d03v + lv) >> 1);
-				c_even = yuv_rgb(y_even, near_a ? (d03u + tu) >> 1 : (d12u + uu) >> 1, near_a ? (d03v + tv) >> 1 : (d12v + uv) >> 1);
-			};
-			for (uint32_t g0 = gu0 + kGroup * tid; g0 < gu1; g0 += kGroup * kThreads) {
-				// (row, unit) of the group's first unit = divmod(g0, UPR): float estimate + corrections
-				int y0 = (int)((float)g0 * inv);
-				int k0 = (int)g0 - y0 * (int)UPR;
-				while (k0 < 0) k0 += (int)UPR, y0--;
-				while (k0 >= (int)UPR) k0 -= (int)UPR, y0++;
-				const uint32_t a0 = y0 ? (uint32_t)(y0 - 1) >> 1 : 0u, b0 = y0 ? min(a0 + 1u, ch - 1u) : 0u;
-				const bool near0 = y0 == 0 || (y0 & 1);
-				// fast group: 4 inner units of one row (8 pixels, 24 contiguous bytes of one stored block)
-				// inside the span
-				const uint32_t p0 = (uint32_t)y0 * SB + f + 3u * (2u * (uint32_t)k0 - 1u);
-				const uint32_t q0 = png ? kPngRaw0 + p0 + 5u * (p0 / kBlk) : d.prefix_len + p0;
-				const bool fast = k0 >= 1 && 2u * ((uint32_t)k0 + kGroup - 1u) < W && g0 + kGroup <= gu1 &&
-				                  (!png || p0 / kBlk == (p0 + 3u * 2u * kGroup - 1u) / kBlk) && q0 >= F0 &&
-				                  q0 + 3u * 2u * kGroup <= F0 + kSpan;
-				if (fast) {
-					// chroma columns k0-1 .. k0+3 of rows a, b; luma x = 2k0-1 .. 2k0+6 (32-bit offsets
-					// from the uniform plane bases)
-					const uint32_t ua = a0 * d.stride_uv + (uint32_t)k0 - 1u, ub = b0 * d.stride_uv + (uint32_t)k0 - 1u;
-					const uint32_t yo = (uint32_t)y0 * d.stride_y + 2u * (uint32_t)k0 - 1u;
-					int ca[5], cb[5], va[5], vb[5], yv[8];
-#pragma unroll
-					for (int j = 0; j < 5; j++) ca[j] = U[ua + j], cb[j] = U[ub + j], va[j] = V[ua + j], vb[j] = V[ub + j];
-#pragma unroll
-					for (int j = 0; j < 8; j++) yv[j] = Y[yo + j];
-					uint8_t* o = L.buf + (q0 - F0);
-#pragma unroll
-					for (int i = 0; i < (int)kGroup; i++) {
-						uint32_t c_odd, c_even;
-						pair_rgb(near0, ca[i], ca[i + 1], cb[i], cb[i + 1], va[i], va[i + 1], vb[i], vb[i + 1], yv[2 * i],
-						         yv[2 * i + 1], c_odd, c_even);
-						o[6 * i + 0] = (uint8_t)c_odd, o[6 * i + 1] = (uint8_t)(c_odd >> 8), o[6 * i + 2] = (uint8_t)(c_odd >> 16);
-						o[6 * i + 3] = (uint8_t)c_even, o[6 * i + 4] = (uint8_t)(c_even >> 8), o[6 * i + 5] = (uint8_t)(c_even >> 16);
-					}
-					continue;
-				}
-				// generic units (row ends, span / block boundaries, narrow images)
-				for (uint32_t j = 0; j < kGroup; j++) {
-					if (g0 + j >= gu1) break;
-					int y = y0, k = k0 + (int)j;
-					while (k >= (int)UPR) k -= (int)UPR, y++;
-					const uint32_t a = y ? (uint32_t)(y - 1) >> 1 : 0u, b = y ? min(a + 1u, ch - 1u) : 0u;
-					const bool near_a = y == 0 || (y & 1);
-					const uint32_t cl = k ? (uint32_t)k - 1u : 0u, cr = min((uint32_t)k, cw - 1u);
-					const uint32_t ra = a * d.stride_uv, rb = b * d.stride_uv, yr = (uint32_t)y * d.stride_y;
-					const bool has_odd = k > 0, has_even = 2u * (uint32_t)k < W;
-					uint32_t c_odd, c_even;
-					// (indices clamped so that no load leaves the plane)
-					pair_rgb(near_a, U[ra + cl], U[ra + cr], U[rb + cl], U[rb + cr], V[ra + cl], V[ra + cr], V[rb + cl],
-					         V[rb + cr], Y[yr + (k ? 2u * (uint32_t)k - 1u : 0u)], Y[yr + min(2u * (uint32_t)k, W - 1u)], c_odd,
-					         c_even);
-					// bytes: [filter byte (PNG, k == 0)] [odd pixel] [even pixel], from raw offset pb
-					const uint32_t rowp = (uint32_t)y * SB;
-					const uint32_t pb = k ? rowp + f + 3u * (2u * (uint32_t)k - 1u) : rowp;
-					const uint32_t nb = (k ? 0u : f) + (has_odd ? 3u : 0u) + (has_even ? 3u : 0u);
-					uint32_t qb, bnd = 0xFFFFFFFFu;
-					if (png) {
-						const uint32_t blk = pb / kBlk;
-						qb = kPngRaw0 + pb + 5u * blk;
-						bnd = (blk + 1u) * kBlk;  // raw offset where the next block header intervenes
-					} else {
-						qb = d.prefix_len + pb;
-					}
-					const uint64_t bytes = k ? ((uint64_t)c_even << 24) | c_odd : (f ? ((uint64_t)c_even << 8) : (uint64_t)c_even);
-					for (uint32_t i = 0; i < nb; i++) {
-						const uint32_t q = qb + i + ((pb + i >= bnd) ? 5u : 0u) - F0;
-						if (q < kSpan) L.buf[q] = (uint8_t)(bytes >> (8 * i));
-					}
-				}
-			}
-		}
-		// -- 1b. layout bytes in the span
-		if (tid < 64) {
-			// prefix (PPM header / PNG signature + IHDR + IDAT header + zlib header)
-			if (tid < d.prefix_len && tid >= F0 && tid < F0 + kSpan) L.buf[tid - F0] = d.prefix[tid];
-		} else if (png && tid < 74) {
-			// stored-block headers: at most two blocks meet a span
-			const uint32_t j = tid - 64, kc = (F0 >= kPngPrefix ? (F0 - kPngPrefix) / kBlkFile : 0u) + j / 5u;
-			const uint32_t q = kPngPrefix + kc * kBlkFile + j % 5u;
-			const uint32_t nblk = (d.raw_len + kBlk - 1u) / kBlk;
-			if (kc < nblk && q >= F0 && q < F0 + kSpan) {
-				const uint32_t len = min(kBlk, d.raw_len - kc * kBlk);
-				const uint32_t hdr[5] = {kc + 1u == nblk ? 1u : 0u, len & 255u, len >> 8, ~len & 255u, (~len >> 8) & 255u};
-				L.buf[q - F0] = (uint8_t)hdr[j % 5u];
-			}
-		} else if (png && tid >= 96 && tid < 116) {
-			// Adler-32 and CRC placeholders (written by the finishing launch), IEND chunk
-			const uint32_t i = tid - 96, q = d.zend - 4u + i;
-			const uint8_t iend[12] = {0, 0, 0, 0, 'I', 'E', 'N', 'D', 0xAE, 0x42, 0x60, 0x82};
-			if (q >= F0 && q < F0 + kSpan) L.buf[q - F0] = i < 8 ? 0 : iend[i - 8];
-		} else if (tid >= 128 && tid < 144) {
-			// alignment padding after the file (the last 16-byte store covers it)
-			const uint32_t q = flen + (tid - 128);
-			if (q >= F0 && q < F0 + kSpan && q < ((flen + 15u) & ~15u)) L.buf[q - F0] = 0;
-		}
-		__syncthreads();
-
-		// -- 2. stream 64 contiguous bytes per thread to HBM (+ PNG checksum partials)
 		const uint32_t q0 = F0 + tid * kPerThread;
-		const uint32_t* bw = (const uint32_t*)(L.buf + tid * kPerThread);
-		uint8_t* dst = out + d.out + q0;
-#pragma unroll
-		for (uint32_t i = 0; i < kPerThread / 16u; i++)
-			if (q0 + 16u * i < flen) *(uint4*)(dst + 16u * i) = *(const uint4*)(bw + 4u * i);
-		if (png) {
+		{
 			uint32_t c = 0, s0 = 0, s1 = 0;
 			const uint32_t N = d.raw_len;
 			const uint32_t z0 = q0 - kPngPrefix, k0 = z0 / kBlkFile, o0 = z0 - k0 * kBlkFile;
 			const uint32_t p0 = k0 * kBlk + o0 - 5u;
 			const bool fast = q0 >= kPngRaw0 && o0 >= 5u && o0 + kPerThread <= kBlkFile && p0 + kPerThread <= N;
 			if (fast) {
-				// all 64 bytes are pixel-stream bytes of one stored block (inside the CRC range)
+				// all 32 bytes are pixel-stream bytes of one stored block (inside the CRC range)
 				uint32_t sj = 0;
 #pragma unroll
 				for (uint32_t i = 0; i < kPerThread / 4u; i += 2) {
@@ -276,8 +290,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8, 8))
 				s0 %= kMod;
 			} else if (q0 < d.zend + 4u) {
 				const uint32_t crc_end = d.zend - 4u, raw_end = png_file_of_raw(N - 1u) + 1u;
+#pragma unroll
 				for (uint32_t j = 0; j < kPerThread; j++) {
-					const uint32_t q = q0 + j, v = L.buf[tid * kPerThread + j];
+					const uint32_t q = q0 + j, v = (bw[j >> 2] >> (8 * (j & 3))) & 255u;
 					c = crc_byte(L.tab, c, (q >= kCrcStart && q < crc_end) ? v : 0u);
 					if (q >= kPngRaw0 && q < raw_end) {
 						const uint32_t z = q - kPngPrefix, k = z / kBlkFile, o = z - k * kBlkFile;
@@ -293,25 +308,78 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8, 8))
 #pragma unroll
 				for (uint32_t i = 0; i < kPerThread / 4u; i += 2) c = crc_dword2(L.tab, c, 0u, 0u);
 			}
-			// -- 3. span CRC: tree over the 512 thread CRCs (each over 64 bytes)
-			L.red[0][tid] = c;
-			L.red[1][tid] = s0;
-			L.red[2][tid] = s1;
-			for (int l = 0; l < kTreeLevels; l++) {
-				__syncthreads();
-				if (tid < (uint32_t)(kThreads >> (l + 1))) {
-					const uint32_t lo = tid << (l + 1), hi = lo + (1u << l);
-					L.red[0][lo] = nib_apply(L.tab + kNibBase + l * 128, L.red[0][lo]) ^ L.red[0][hi];
-					L.red[1][lo] = (L.red[1][lo] + L.red[1][hi]) % kMod;
-					L.red[2][lo] = (L.red[2][lo] + L.red[2][hi]) % kMod;
+			// -- 3. span CRC: tree over the 1024 thread CRCs (32 bytes each): levels 0..5 inside the
+			// wave (lane shuffles), then one partial per wave through LDS and levels 6..9 in wave 0.
+			// crc(lo || hi) = Z_|hi|(crc(lo)) ^ crc(hi); the Adler partials just add.
+			const uint32_t lane = tid & 63u, wv = tid >> 6, par = tcount & 1u;
+#pragma unroll
+			for (int l = 0; l < 6; l++) {
+				const uint32_t oc = __shfl_down(c, 1u << l, 64), o0 = __shfl_down(s0, 1u << l, 64), o1 = __shfl_down(s1, 1u << l, 64);
+				c = nib_apply(L.tab + kNibBase + l * 128, c) ^ oc;
+				s0 = mod_add(s0, o0);
+				s1 = mod_add(s1, o1);
+			}
+			if (lane == 0) L.red[par][0][wv] = c, L.red[par][1][wv] = s0, L.red[par][2][wv] = s1;
+			__syncthreads();
+			if (wv == 0) {
+				c = lane < 16u ? L.red[par][0][lane] : 0u;
+				s0 = lane < 16u ? L.red[par][1][lane] : 0u;
+				s1 = lane < 16u ? L.red[par][2][lane] : 0u;
+#pragma unroll
+				for (int l = 6; l < kTreeLevels; l++) {
+					const uint32_t sh = 1u << (l - 6);
+					const uint32_t oc = __shfl_down(c, sh, 16), o0 = __shfl_down(s0, sh, 16), o1 = __shfl_down(s1, sh, 16);
+					c = nib_apply(L.tab + kNibBase + l * 128, c) ^ oc;
+					s0 = mod_add(s0, o0);
+					s1 = mod_add(s1, o1);
+				}
+				if (lane == 0) {
+					uint32_t* pp = part + 4u * g;
+					pp[0] = c;
+					pp[1] = s0;
+					pp[2] = s1;
 				}
 			}
-			if (tid == 0) {
-				uint32_t* pp = part + 4u * g;
-				pp[0] = L.red[0][0];
-				pp[1] = L.red[1][0];
-				pp[2] = L.red[2][0];
+			tcount++;
+		}
+	}
+}
+
+// ---- write kernel (every format): the file bytes of one 32 KB span per workgroup task, straight
+// to HBM -- pixel bytes with unaligned 8-byte stores (full lines form in L2 from neighbouring
+// threads), layout bytes one by one.  No LDS image and no barriers, so the waves of a CU overlap
+// their loads freely.
+constexpr int kPlainThreads = 256;
+__global__ __launch_bounds__(kPlainThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void enc_write_kernel(const Vp8gEncDesc* __restrict__ D, uint32_t n,
+                                                                  uint32_t total, const uint8_t* __restrict__ src,
+                                                                  uint8_t* __restrict__ out) {
+	const uint32_t tid = threadIdx.x;
+	uint32_t img = 0;
+	for (uint32_t g = blockIdx.x; g < total; g += gridDim.x) {
+		while (img + 1 < n && D[img + 1].span0 <= g) img++;  // tasks are numbered image by image
+		const Vp8gEncDesc& d = D[img];
+		const bool png = d.format == VP8G_ENC_PNG;
+		const uint32_t F0 = (g - d.span0) * kSpan;
+		uint8_t* file = out + d.out;
+		span_pixels<kPlainThreads>(d, png, F0, tid, src, file);
+		if (tid < 64) {
+			// prefix (PPM header / PNG signature + IHDR + IDAT header + zlib header)
+			if (tid < d.prefix_len && tid >= F0 && tid < F0 + kSpan) file[tid] = d.prefix[tid];
+		} else if (png && tid < 74) {
+			// stored-block headers: at most two blocks meet a span
+			const uint32_t j = tid - 64, kc = (F0 >= kPngPrefix ? (F0 - kPngPrefix) / kBlkFile : 0u) + j / 5u;
+			const uint32_t q = kPngPrefix + kc * kBlkFile + j % 5u;
+			const uint32_t nblk = (d.raw_len + kBlk - 1u) / kBlk;
+			if (kc < nblk && q >= F0 && q < F0 + kSpan) {
+				const uint32_t len = min(kBlk, d.raw_len - kc * kBlk);
+				const uint32_t hdr[5] = {kc + 1u == nblk ? 1u : 0u, len & 255u, len >> 8, ~len & 255u, (~len >> 8) & 255u};
+				file[q] = (uint8_t)hdr[j % 5u];
 			}
+		} else if (png && tid >= 96 && tid < 116) {
+			// Adler-32 and CRC placeholders (written by the finishing launch), IEND chunk
+			const uint32_t i = tid - 96, q = d.zend - 4u + i;
+			const uint8_t iend[12] = {0, 0, 0, 0, 'I', 'E', 'N', 'D', 0xAE, 0x42, 0x60, 0x82};
+			if (q >= F0 && q < F0 + kSpan) file[q] = i < 8 ? 0 : iend[i - 8];
 		}
 	}
 }
@@ -590,11 +658,18 @@ VP8G_API int vp8g_encode_batch_device(const Vp8gEncDesc* h, const Vp8gEncDesc* d
 		any_png |= h[i].format == VP8G_ENC_PNG;
 	}
 	uint32_t* tab = nullptr;
-	hipError_t e = tables_dev(&tab);
-	if (e == hipSuccess) {
-		const int cus = vp8g::device_cus();
+	const int cus = vp8g::device_cus();
+	hipError_t e = hipSuccess;
+	{
+		const uint32_t grid = min(total, (uint32_t)(cus > 0 ? cus : 256) * 16u);
+		hipLaunchKernelGGL(enc_write_kernel, dim3(grid), dim3(kPlainThreads), 0, (hipStream_t)stream, d_descs, n, total, d_src,
+		                   d_out);
+		e = hipGetLastError();
+	}
+	if (e == hipSuccess && any_png) e = tables_dev(&tab);
+	if (e == hipSuccess && any_png) {
 		const uint32_t grid = min(total, (uint32_t)(cus > 0 ? cus : 256) * 4u);
-		hipLaunchKernelGGL(enc_kernel, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, d_descs, n, total, d_src, d_out,
+		hipLaunchKernelGGL(crc_kernel, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, d_descs, n, total, d_out,
 		                   (uint32_t*)d_work, tab);
 		e = hipGetLastError();
 	}
