@@ -223,6 +223,25 @@ typedef struct {
 	uint64_t n_values;
 } Vp8gPackedFrame;
 
+/* Device m05 job of one frame: the host parses the frame header and the
+ * first partition's frame-level fields (RFC 6386 9.2-9.11, 13.4); the device decodes the
+ * per-macroblock modes (partition 0, from the saved bool-decoder state) and the coefficient
+ * tokens (the token partition) into the batch SoA of Vp8gBatchArrays.  1216 bytes. */
+typedef struct {
+	uint64_t data;       /* byte offset of the VP8 payload in the device bitstream buffer (caller) */
+	uint64_t mb_offset;  /* first MB of the frame in the batch arrays (caller) */
+	uint64_t b_value;    /* partition-0 bool decoder at the first MB header: value window, */
+	int32_t b_bits;      /*   bits below the 8-bit comparison window, */
+	uint32_t b_range;    /*   range (128..255), */
+	uint32_t b_next;     /*   payload offset of the next byte to load */
+	uint32_t p0_end;     /* payload offset one past the first partition (bytes beyond read as 0) */
+	uint32_t tok_off, tok_end; /* the token partition [tok_off, tok_end) of the payload */
+	uint32_t mb_cols, mb_rows;
+	uint8_t seg_enabled, seg_map_update, use_skip, skip_prob;
+	uint8_t seg_probs[3], reserved;
+	uint8_t coeff_probs[4][8][3][12]; /* RFC 13.4 after this frame's updates; rows padded to 12 */
+} Vp8gTokFrame;
+
 /* Decode n .webp file images end to end: container/header/m05 on `threads` host threads (0 = the
  * CPUs this process may run on) into the packed format, chunks of frames uploaded packed,
  * expanded and reconstructed (+ loop filter when `filtered`) on the device while the next chunk

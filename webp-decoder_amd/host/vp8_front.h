@@ -52,6 +52,11 @@ int vp8f_decode_packed(ByteSpan vp8_payload, Vp8gPackedFrame* out, unsigned flag
 int vp8f_decode_packed_memory(const uint8_t* data, size_t size, Vp8gPackedFrame* out, int* stage, unsigned flags);
 void vp8f_packed_free(Vp8gPackedFrame* p);
 
+/* Host half of the device m05 (Vp8gTokFrame, include/vp8g.h): key-frame header + the first
+ * partition's frame-level fields; hdr receives those fields (no arrays), tf the device job
+ * (data / mb_offset left 0 for the caller).  0, or -1 + errno (EINVAL, ENOTSUP). */
+int vp8f_token_header(ByteSpan vp8_payload, Vp8KeyFrameHeader* kf, Vp8DecodedFrame* hdr, Vp8gTokFrame* tf);
+
 /* Seeded synthetic Vp8DecodedFrame (build-defined generator, see vp8_synth.c header for the
  * exact distribution).  profile 0 = "measured-like" statistics, 1 = stress (full-range coeffs,
  * all modes uniformly, random LF/segment parameters).  kf receives width/height. */

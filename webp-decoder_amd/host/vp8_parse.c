@@ -310,6 +310,76 @@ static int8_t read_opt_signed(Vp8Bool* b, int nbits) {
 	return clamp_s8(vp8b_signed(b, nbits));
 }
 
+/* Frame-level fields of the first partition (RFC 6386 9.3-9.11, 13.4): everything before the
+ * first macroblock header.  Leaves h->hb at the first macroblock header. */
+typedef struct {
+	Vp8Bool hb;
+	int seg_map_update;
+	uint8_t seg_probs[3];
+	int use_skip;
+	uint8_t skip_prob;
+	unsigned nparts;
+	uint8_t probs[4][8][3][11];
+} FrameHdr;
+
+static void parse_frame_header(ByteSpan payload, const Vp8KeyFrameHeader* kf, Vp8DecodedFrame* out, FrameHdr* h) {
+	Vp8Bool* const hb = &h->hb;
+	vp8b_init(hb, payload.data + 10, kf->first_partition_len);
+	out->stats.part0_size_bytes = kf->first_partition_len;
+	(void)vp8b_read(hb, 128); /* color space */
+	(void)vp8b_read(hb, 128); /* clamping type */
+
+	/* RFC 6386 9.3 segmentation */
+	h->seg_map_update = 0;
+	h->seg_probs[0] = h->seg_probs[1] = h->seg_probs[2] = 255;
+	out->segmentation_enabled = (uint8_t)vp8b_read(hb, 128);
+	if (out->segmentation_enabled) {
+		h->seg_map_update = vp8b_read(hb, 128);
+		if (vp8b_read(hb, 128)) { /* update_segment_feature_data */
+			out->segmentation_abs = (uint8_t)vp8b_read(hb, 128);
+			for (int i = 0; i < 4; i++) out->seg_quant_idx[i] = read_opt_signed(hb, 7);
+			for (int i = 0; i < 4; i++) out->seg_lf_level[i] = read_opt_signed(hb, 6);
+		}
+		if (h->seg_map_update)
+			for (int i = 0; i < 3; i++)
+				if (vp8b_read(hb, 128)) h->seg_probs[i] = (uint8_t)vp8b_literal(hb, 8);
+	}
+
+	/* RFC 6386 9.6 loop filter */
+	out->lf_use_simple = (uint8_t)vp8b_read(hb, 128);
+	out->lf_level = (uint8_t)vp8b_literal(hb, 6);
+	out->lf_sharpness = (uint8_t)vp8b_literal(hb, 3);
+	out->lf_delta_enabled = (uint8_t)vp8b_read(hb, 128);
+	if (out->lf_delta_enabled && vp8b_read(hb, 128)) {
+		for (int i = 0; i < 4; i++) out->lf_ref_delta[i] = read_opt_signed(hb, 6);
+		for (int i = 0; i < 4; i++) out->lf_mode_delta[i] = read_opt_signed(hb, 6);
+	}
+
+	/* RFC 6386 9.5 token partitions */
+	h->nparts = 1u << vp8b_literal(hb, 2);
+
+	/* RFC 6386 9.6 quantisation */
+	out->q_index = (uint8_t)vp8b_literal(hb, 7);
+	out->y1_dc_delta_q = read_opt_signed(hb, 4);
+	out->y2_dc_delta_q = read_opt_signed(hb, 4);
+	out->y2_ac_delta_q = read_opt_signed(hb, 4);
+	out->uv_dc_delta_q = read_opt_signed(hb, 4);
+	out->uv_ac_delta_q = read_opt_signed(hb, 4);
+	(void)vp8b_read(hb, 128); /* refresh_entropy_probs */
+
+	/* RFC 6386 13.4 token probability updates */
+	memcpy(h->probs, vp8_default_coeff_probs, sizeof(h->probs));
+	for (int i = 0; i < 4; i++)
+		for (int j = 0; j < 8; j++)
+			for (int k = 0; k < 3; k++)
+				for (int l = 0; l < 11; l++)
+					if (vp8b_read(hb, vp8_coeff_update_probs[i][j][k][l])) h->probs[i][j][k][l] = (uint8_t)vp8b_literal(hb, 8);
+
+	h->use_skip = vp8b_read(hb, 128);
+	h->skip_prob = h->use_skip ? (uint8_t)vp8b_literal(hb, 8) : 0;
+
+}
+
 static int decode_frame(ByteSpan payload, Vp8DecodedFrame* out, Sink* sk) {
 	if (!out) return -1;
 	memset(out, 0, sizeof(*out));
@@ -371,60 +441,14 @@ static int decode_frame(ByteSpan payload, Vp8DecodedFrame* out, Sink* sk) {
 		goto done;
 	}
 
-	Vp8Bool hb;
-	vp8b_init(&hb, payload.data + 10, kf.first_partition_len);
-	st->part0_size_bytes = kf.first_partition_len;
-	(void)vp8b_read(&hb, 128); /* color space */
-	(void)vp8b_read(&hb, 128); /* clamping type */
-
-	/* RFC 6386 9.3 segmentation */
-	int seg_map_update = 0;
-	uint8_t seg_probs[3] = {255, 255, 255};
-	out->segmentation_enabled = (uint8_t)vp8b_read(&hb, 128);
-	if (out->segmentation_enabled) {
-		seg_map_update = vp8b_read(&hb, 128);
-		if (vp8b_read(&hb, 128)) { /* update_segment_feature_data */
-			out->segmentation_abs = (uint8_t)vp8b_read(&hb, 128);
-			for (int i = 0; i < 4; i++) out->seg_quant_idx[i] = read_opt_signed(&hb, 7);
-			for (int i = 0; i < 4; i++) out->seg_lf_level[i] = read_opt_signed(&hb, 6);
-		}
-		if (seg_map_update)
-			for (int i = 0; i < 3; i++)
-				if (vp8b_read(&hb, 128)) seg_probs[i] = (uint8_t)vp8b_literal(&hb, 8);
-	}
-
-	/* RFC 6386 9.6 loop filter */
-	out->lf_use_simple = (uint8_t)vp8b_read(&hb, 128);
-	out->lf_level = (uint8_t)vp8b_literal(&hb, 6);
-	out->lf_sharpness = (uint8_t)vp8b_literal(&hb, 3);
-	out->lf_delta_enabled = (uint8_t)vp8b_read(&hb, 128);
-	if (out->lf_delta_enabled && vp8b_read(&hb, 128)) {
-		for (int i = 0; i < 4; i++) out->lf_ref_delta[i] = read_opt_signed(&hb, 6);
-		for (int i = 0; i < 4; i++) out->lf_mode_delta[i] = read_opt_signed(&hb, 6);
-	}
-
-	/* RFC 6386 9.5 token partitions */
-	const unsigned nparts = 1u << vp8b_literal(&hb, 2);
-
-	/* RFC 6386 9.6 quantisation */
-	out->q_index = (uint8_t)vp8b_literal(&hb, 7);
-	out->y1_dc_delta_q = read_opt_signed(&hb, 4);
-	out->y2_dc_delta_q = read_opt_signed(&hb, 4);
-	out->y2_ac_delta_q = read_opt_signed(&hb, 4);
-	out->uv_dc_delta_q = read_opt_signed(&hb, 4);
-	out->uv_ac_delta_q = read_opt_signed(&hb, 4);
-	(void)vp8b_read(&hb, 128); /* refresh_entropy_probs */
-
-	/* RFC 6386 13.4 token probability updates */
-	memcpy(t->probs, vp8_default_coeff_probs, sizeof(t->probs));
-	for (int i = 0; i < 4; i++)
-		for (int j = 0; j < 8; j++)
-			for (int k = 0; k < 3; k++)
-				for (int l = 0; l < 11; l++)
-					if (vp8b_read(&hb, vp8_coeff_update_probs[i][j][k][l])) t->probs[i][j][k][l] = (uint8_t)vp8b_literal(&hb, 8);
-
-	const int use_skip = vp8b_read(&hb, 128);
-	const uint8_t skip_prob = use_skip ? (uint8_t)vp8b_literal(&hb, 8) : 0;
+	FrameHdr fh;
+	parse_frame_header(payload, &kf, out, &fh);
+	Vp8Bool hb = fh.hb;
+	const int seg_map_update = fh.seg_map_update, use_skip = fh.use_skip;
+	const uint8_t* const seg_probs = fh.seg_probs;
+	const uint8_t skip_prob = fh.skip_prob;
+	const unsigned nparts = fh.nparts;
+	memcpy(t->probs, fh.probs, sizeof(t->probs));
 
 	/* RFC 6386 11 / 19.3 per-macroblock header */
 	for (uint32_t r = 0; r < rows; r++) {
@@ -520,6 +544,51 @@ int vp8f_decode_packed(ByteSpan payload, Vp8gPackedFrame* out, unsigned flags) {
 		return -1;
 	}
 	return decode_frame(payload, &out->f, &sk);
+}
+
+int vp8f_token_header(ByteSpan payload, Vp8KeyFrameHeader* kf, Vp8DecodedFrame* hdr, Vp8gTokFrame* tf) {
+	if (!kf || !hdr || !tf) {
+		errno = EINVAL;
+		return -1;
+	}
+	memset(hdr, 0, sizeof(*hdr));
+	memset(tf, 0, sizeof(*tf));
+	if (vp8_parse_keyframe_header(payload, kf) != 0) {
+		errno = EINVAL;
+		return -1;
+	}
+	const uint32_t cols = (kf->width + 15u) >> 4, rows = (kf->height + 15u) >> 4;
+	if (cols == 0 || rows == 0 || cols * rows > (1u << 20) || payload.size < 10u + kf->first_partition_len) {
+		errno = EINVAL;
+		return -1;
+	}
+	hdr->mb_cols = hdr->stats.mb_cols = cols;
+	hdr->mb_rows = hdr->stats.mb_rows = rows;
+	hdr->mb_total = hdr->stats.mb_total = cols * rows;
+	FrameHdr fh;
+	parse_frame_header(payload, kf, hdr, &fh);
+	if (fh.nparts != 1) { /* the reference's m05 supports one token partition (vp8_tokens.c:357-360) */
+		errno = ENOTSUP;
+		return -1;
+	}
+	tf->mb_cols = cols;
+	tf->mb_rows = rows;
+	tf->p0_end = 10u + kf->first_partition_len;
+	tf->tok_off = tf->p0_end;
+	tf->tok_end = (uint32_t)payload.size;
+	tf->b_next = (uint32_t)(fh.hb.next - payload.data);
+	tf->b_value = fh.hb.value;
+	tf->b_bits = fh.hb.bits;
+	tf->b_range = fh.hb.range;
+	tf->seg_enabled = hdr->segmentation_enabled;
+	tf->seg_map_update = (uint8_t)fh.seg_map_update;
+	tf->use_skip = (uint8_t)fh.use_skip;
+	tf->skip_prob = fh.skip_prob;
+	memcpy(tf->seg_probs, fh.seg_probs, 3);
+	for (int i = 0; i < 4; i++)
+		for (int j = 0; j < 8; j++)
+			for (int k = 0; k < 3; k++) memcpy(tf->coeff_probs[i][j][k], fh.probs[i][j][k], 11);
+	return 0;
 }
 
 void vp8f_packed_free(Vp8gPackedFrame* p) {
