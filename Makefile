@@ -15,7 +15,7 @@ OFFLOAD_ARCH ?= gfx950
 
 HOST_SRC := $(PKG)/host/webp_riff.c $(PKG)/host/vp8_parse.c $(PKG)/host/vp8_synth.c
 HOST_HDR := $(PKG)/host/vp8_front.h $(PKG)/host/vp8_bool.h $(PKG)/host/vp8_tables.inc include/vp8g.h
-HIP_SRC := $(PKG)/csrc/vp8g_kernels.hip $(PKG)/csrc/vp8g_shim.hip $(PKG)/csrc/vp8g_rgb.hip $(PKG)/csrc/vp8g_pipeline.hip
+HIP_SRC := $(PKG)/csrc/vp8g_kernels.hip $(PKG)/csrc/vp8g_shim.hip $(PKG)/csrc/vp8g_rgb.hip $(PKG)/csrc/vp8g_pipeline.hip $(PKG)/csrc/vp8g_m05.hip
 HIP_HDR := $(PKG)/csrc/vp8g_device.h include/vp8g.h $(PKG)/host/vp8_front.h
 # libvp8g links the host front end (the end-to-end batch path runs m05 on worker threads)
 HIP_LINK := -L$(LIB) -lvp8host -Wl,-rpath,'$$ORIGIN' -lpthread

@@ -252,6 +252,21 @@ typedef struct {
 int vp8g_decode_webp_batch(const ByteSpan* files, uint32_t n, int filtered, uint32_t threads, Yuv420Image* outs,
                            int* status);
 
+/* vp8g_decode_webp_batch with options.  VP8G_BATCH_DEVICE_M05: the host threads only parse the
+ * container and the frame headers; the compressed payloads are uploaded and m05 runs on the
+ * device (vp8g_m05_batch_device), one wavefront per frame.  Same outputs and errors. */
+#define VP8G_BATCH_DEVICE_M05 1u
+int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int filtered, uint32_t threads, uint32_t flags,
+                              Yuv420Image* outs, int* status);
+
+/* Device m05 over n frames on `hip_stream`: h_jobs / d_jobs host and device copies of the jobs
+ * (data = payload offset in d_bits, 4-aligned, with >= 8 readable bytes after the payload;
+ * mb_offset = first MB in the arrays).  Writes ymode, uv_mode, segment_id, has_coeff, bmode and
+ * the non-zero coefficients of `arrays` (the caller zeroes the four coefficient arrays first).
+ * Asynchronous; 0 or -1 + errno (EINVAL for an inconsistent job, EIO on a launch failure). */
+int vp8g_m05_batch_device(const Vp8gTokFrame* h_jobs, const Vp8gTokFrame* d_jobs, uint32_t n, const uint8_t* d_bits,
+                          const Vp8gBatchArrays* arrays, void* hip_stream);
+
 /* ---- m08 / m09 boundary: I420 -> RGB24 ("fancy" 4:2:0 upsampling) and the file writers -- */
 
 /* replaces src/m08_yuv2rgb_ppm/yuv2rgb_ppm.c:123 (decl yuv2rgb_ppm.h:10): binary PPM (P6) of img
@@ -313,7 +328,7 @@ int vp8g_encode_batch_device(const Vp8gEncDesc* h_descs, const Vp8gEncDesc* d_de
 const char* vp8g_last_error(void);
 
 /* ABI version of this header (bumped on any layout change). */
-#define VP8G_ABI_VERSION 3
+#define VP8G_ABI_VERSION 4
 uint32_t vp8g_abi_version(void);
 
 #ifdef __cplusplus

@@ -108,3 +108,42 @@ def test_front_end_stats_equal_reference_on_truncated_streams(vp8g, manifest, tm
                 ref.ref_free_frame(C.byref(rf))
                 host.vp8_decoded_frame_free(C.byref(df))
     assert n_ovr > 10  # the truncations did reach the overread paths
+
+
+def test_token_header_matches_front_end(vp8g, manifest):
+    """vp8f_token_header_memory (host half of the device m05): the frame-level fields equal the
+    full front end's, the job locates the partitions inside the VP8 payload and starts partition 0's
+    bool decoder in a valid state."""
+    import ctypes as C
+    import struct
+    host = vp8g.host_lib()
+    hdr_fields = [n for n, _ in vp8g.Vp8DecodedFrame._fields_ if not n.startswith(("segment_id", "skip", "has_",
+                  "ymode", "uv_mode", "bmode", "coeff", "stats"))]
+    for rel in sorted(manifest["files"])[::3]:
+        data = (FIXTURES / rel).read_bytes()
+        kf, hdr, tf, off, size = vp8g.token_header(data)
+        assert off == 20 and size == struct.unpack("<I", data[16:20])[0]
+        kf2, df, st = vp8g.Vp8KeyFrameHeader(), vp8g.Vp8DecodedFrame(), C.c_int(0)
+        buf = (C.c_uint8 * len(data)).from_buffer_copy(data)
+        assert host.vp8f_decode_memory(buf, len(data), C.byref(kf2), C.byref(df), C.byref(st)) == 0
+        try:
+            assert bytes(kf) == bytes(kf2)
+            for n in hdr_fields:
+                a, b = getattr(hdr, n), getattr(df, n)
+                assert (list(a) if hasattr(a, "__len__") else a) == (list(b) if hasattr(b, "__len__") else b), (rel, n)
+            assert (tf.mb_cols, tf.mb_rows) == (df.mb_cols, df.mb_rows)
+            assert tf.p0_end == 10 + kf.first_partition_len == tf.tok_off and tf.tok_end == size
+            assert 128 <= tf.b_range <= 255 and 0 <= tf.b_bits <= 56 and 10 < tf.b_next <= tf.p0_end
+            assert tf.seg_enabled == df.segmentation_enabled
+            probs = np.frombuffer(bytes(tf.coeff_probs), np.uint8).reshape(4, 8, 3, 12)
+            assert (probs[..., 11] == 0).all()  # the pad byte of each 12-byte row
+        finally:
+            host.vp8_decoded_frame_free(C.byref(df))
+
+
+def test_token_header_rejects(vp8g):
+    for name in ("empty_riff.webp", "truncated.webp"):
+        with pytest.raises(ValueError):
+            vp8g.token_header((ROOT / "tests" / "fixtures_err" / name).read_bytes())
+    with pytest.raises(ValueError):
+        vp8g.token_header(b"")

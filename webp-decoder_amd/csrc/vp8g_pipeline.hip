@@ -10,6 +10,11 @@
 //                    into the callers' images.  Two chunk slots alternate, so the device work and
 //                    the copies of one chunk overlap the entropy decoding of the next ones.
 //
+// With VP8G_BATCH_DEVICE_M05 the workers only parse the container, the
+// frame header and the first partition's frame-level fields (vp8f_token_header_memory); the
+// chunk uploads the compressed VP8 payloads themselves (the smallest possible wire format), and
+// m05 runs on the device (vp8g_m05.hip, one wavefront per frame) straight into the dense SoA.
+//
 // The reference decodes one file per process (src/main.c:591-705: m01..m05 then m06/m07); its
 // m05 keeps global state (vp8_tokens.c:382, :625), which is why it cannot be threaded as is.
 #include <errno.h>
@@ -33,6 +38,10 @@ namespace {
 
 constexpr uint32_t kChunkFrames = 64;          // frames per device chunk (at most)
 constexpr uint64_t kChunkMbs = 2u << 20;       // macroblocks per chunk (at most, unless one frame is bigger)
+// device m05: one wavefront per frame, so a chunk wants many frames (~830 B of device buffers
+// per MB: 16M MBs ~ 13 GB per slot, two slots)
+constexpr uint32_t kTokChunkFrames = 1024;
+constexpr uint64_t kTokChunkMbs = 16u << 20;
 constexpr uint32_t kNb = VP8G_PK_BLOCKS;
 
 // Packed -> dense coefficients.  32 lanes per MB; lane b < 25 owns block b (Y 0..15, U 0..3,
@@ -74,6 +83,18 @@ __global__ __launch_bounds__(256) void expand_kernel(const uint16_t* __restrict_
 }
 
 inline uint64_t al256(uint64_t x) { return (x + 255u) & ~(uint64_t)255u; }
+// bitstream slot of a payload: 16-B aligned start, >= 16 bytes of slack (the device bool
+// decoder reads whole aligned dwords up to 8 bytes past a partition's end)
+inline uint64_t bits_slot(uint32_t psize) { return ((uint64_t)psize + 16u + 15u) & ~(uint64_t)15u; }
+
+// Host half of a device-m05 frame.
+struct TokJob {
+	Vp8KeyFrameHeader kf;
+	Vp8DecodedFrame hdr;  // header fields only (no arrays)
+	Vp8gTokFrame tf;
+	uint64_t poff;  // VP8 payload in the file
+	uint32_t psize;
+};
 
 uint32_t default_threads() {
 	cpu_set_t set;
@@ -89,7 +110,9 @@ uint32_t default_threads() {
 struct Feed {
 	const ByteSpan* files = nullptr;
 	uint32_t n = 0;
+	bool tok = false;  // device m05: workers fill tj instead of pk
 	std::vector<Vp8gPackedFrame> pk;
+	std::vector<TokJob> tj;
 	std::vector<int> err;
 	std::unique_ptr<uint8_t[]> ready;
 	std::atomic<uint32_t> next{0};
@@ -109,7 +132,12 @@ struct Feed {
 			}
 			int stage = 0, e = 0;
 			if (!files[i].data) e = EINVAL;
-			else if (vp8f_decode_packed_memory(files[i].data, files[i].size, &pk[i], &stage, 0) != 0) e = errno ? errno : EINVAL;
+			else if (tok) {
+				TokJob& j = tj[i];
+				if (vp8f_token_header_memory(files[i].data, files[i].size, &j.kf, &j.hdr, &j.tf, &j.poff, &j.psize, &stage) != 0)
+					e = errno ? errno : EINVAL;
+			} else if (vp8f_decode_packed_memory(files[i].data, files[i].size, &pk[i], &stage, 0) != 0)
+				e = errno ? errno : EINVAL;
 			{
 				std::lock_guard<std::mutex> lk(mu);
 				err[i] = e;
@@ -146,11 +174,13 @@ struct Slot {
 	bool busy = false;
 	std::vector<uint32_t> frames;  // frame indices of the chunk (packed data freed when the slot is reused)
 	std::vector<Vp8gFrameDesc> descs;
+	std::vector<Vp8gTokFrame> jobs;  // device m05
 	uint32_t status = 0;
 };
 
 struct ChunkLayout {
-	uint64_t ym, uvm, seg, hasc, bm, masks, mboff, vals, cy, cu, cv, cy2, desc, status, gctx, mbox, gprog, out, total;
+	uint64_t ym, uvm, seg, hasc, bm, masks, mboff, vals, cy, cu, cv, cy2, bits, jobs, desc, status, gctx, mbox, gprog, out,
+	    total;
 };
 
 hipError_t grow(Slot& s, size_t need) {
@@ -166,12 +196,19 @@ hipError_t grow(Slot& s, size_t need) {
 
 }  // namespace
 
-VP8G_API int vp8g_decode_webp_batch(const ByteSpan* files, uint32_t n, int filtered, uint32_t threads, Yuv420Image* outs,
-                                    int* status) {
-	if (!files || !outs || n == 0) {
+VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int filtered, uint32_t threads, uint32_t flags,
+                                       Yuv420Image* outs, int* status) {
+	if (!files || !outs || n == 0 || (flags & ~VP8G_BATCH_DEVICE_M05)) {
 		errno = EINVAL;
 		return -1;
 	}
+	const bool tok = (flags & VP8G_BATCH_DEVICE_M05) != 0;
+	uint32_t chunk_frames = tok ? kTokChunkFrames : kChunkFrames;
+	if (const char* e = getenv("VP8G_CHUNK_FRAMES")) {  // test knob: smaller chunks
+		const long v = atol(e);
+		if (v > 0 && (uint64_t)v < chunk_frames) chunk_frames = (uint32_t)v;
+	}
+	const uint64_t chunk_mbs = tok ? kTokChunkMbs : kChunkMbs;
 	for (uint32_t i = 0; i < n; i++) memset(&outs[i], 0, sizeof(outs[i]));
 	if (!threads) threads = default_threads();
 	if (threads > n) threads = n;
@@ -179,10 +216,12 @@ VP8G_API int vp8g_decode_webp_batch(const ByteSpan* files, uint32_t n, int filte
 	Feed feed;
 	feed.files = files;
 	feed.n = n;
-	feed.pk.assign(n, Vp8gPackedFrame{});
+	feed.tok = tok;
+	if (tok) feed.tj.assign(n, TokJob{});
+	else feed.pk.assign(n, Vp8gPackedFrame{});
 	feed.err.assign(n, 0);
 	feed.ready.reset(new uint8_t[n]());
-	const uint32_t window = 2 * kChunkFrames > 4 * threads ? 2 * kChunkFrames : 4 * threads;
+	const uint32_t window = 2 * chunk_frames > 4 * threads ? 2 * chunk_frames : 4 * threads;
 	feed.limit = window;
 	std::vector<std::thread> pool;
 	pool.reserve(threads);
@@ -194,9 +233,12 @@ VP8G_API int vp8g_decode_webp_batch(const ByteSpan* files, uint32_t n, int filte
 	const char* where = nullptr;
 	hipError_t he = hipSuccess;
 	auto release = [&](Slot& s) {
-		for (uint32_t i : s.frames) vp8f_packed_free(&feed.pk[i]);
+		if (!tok)
+			for (uint32_t i : s.frames) vp8f_packed_free(&feed.pk[i]);
 		s.frames.clear();
 	};
+	auto kf_of = [&](uint32_t i) -> const Vp8KeyFrameHeader& { return tok ? feed.tj[i].kf : feed.pk[i].kf; };
+	auto f_of = [&](uint32_t i) -> const Vp8DecodedFrame& { return tok ? feed.tj[i].hdr : feed.pk[i].f; };
 	auto finish_slot = [&](Slot& s) -> bool {  // wait for a slot's chunk; false on a device failure
 		if (!s.busy) return true;
 		s.busy = false;
@@ -229,17 +271,18 @@ VP8G_API int vp8g_decode_webp_batch(const ByteSpan* files, uint32_t n, int filte
 		while (a < n) {
 			// -- gather the next chunk: consecutive frames, in order, as they finish
 			std::vector<uint32_t> idx;
-			uint64_t mbs = 0, vals = 0, outb = 0;
+			uint64_t mbs = 0, vals = 0, bitsb = 0, outb = 0;
 			uint32_t b = a, max_cols = 0, max_rows = 0;
-			while (b < n && b - a < kChunkFrames) {
+			while (b < n && b - a < chunk_frames) {
 				feed.wait_ready(b);
 				if (feed.err[b] == 0) {
-					const Vp8DecodedFrame& f = feed.pk[b].f;
-					if (!idx.empty() && mbs + f.mb_total > kChunkMbs) break;
+					const Vp8DecodedFrame& f = f_of(b);
+					if (!idx.empty() && mbs + f.mb_total > chunk_mbs) break;
 					idx.push_back(b);
 					mbs += f.mb_total;
-					vals += feed.pk[b].n_values;
-					outb = al256(outb + vp8g_i420_size(feed.pk[b].kf.width, feed.pk[b].kf.height));
+					if (tok) bitsb += bits_slot(feed.tj[b].psize);
+					else vals += feed.pk[b].n_values;
+					outb = al256(outb + vp8g_i420_size(kf_of(b).width, kf_of(b).height));
 					if (f.mb_cols > max_cols) max_cols = f.mb_cols;
 					if (f.mb_rows > max_rows) max_rows = f.mb_rows;
 				}
@@ -264,13 +307,15 @@ VP8G_API int vp8g_decode_webp_batch(const ByteSpan* files, uint32_t n, int filte
 			L.seg = o, o = al256(o + mbs);
 			L.hasc = o, o = al256(o + mbs);
 			L.bm = o, o = al256(o + mbs * 16);
-			L.masks = o, o = al256(o + mbs * kNb * 2);
-			L.mboff = o, o = al256(o + mbs * 4);
-			L.vals = o, o = al256(o + vals * 2 + 64);  // +64: the expansion may address one past the end
+			L.masks = o, o = al256(o + (tok ? 0 : mbs * kNb * 2));
+			L.mboff = o, o = al256(o + (tok ? 0 : mbs * 4));
+			L.vals = o, o = al256(o + (tok ? 0 : vals * 2 + 64));  // +64: the expansion may address one past the end
 			L.cy = o, o = al256(o + mbs * 512);
 			L.cu = o, o = al256(o + mbs * 128);
 			L.cv = o, o = al256(o + mbs * 128);
 			L.cy2 = o, o = al256(o + mbs * 32);
+			L.bits = o, o = al256(o + bitsb);
+			L.jobs = o, o = al256(o + (tok ? nf * sizeof(Vp8gTokFrame) : 0));
 			L.desc = o, o = al256(o + nf * sizeof(Vp8gFrameDesc));
 			L.status = o, o = al256(o + 4);
 			L.gctx = o, o = al256(o + (big ? (uint64_t)nf * max_cols * vp8g::kCtxBytesPerCol : 0));
@@ -282,7 +327,27 @@ VP8G_API int vp8g_decode_webp_batch(const ByteSpan* files, uint32_t n, int filte
 			uint8_t* d = s.buf;
 			// -- descriptors and output images
 			s.descs.assign(nf, Vp8gFrameDesc{});
-			{
+			if (tok) {
+				s.jobs.resize(nf);
+				uint64_t mo = 0, bo = 0, oo = 0;
+				for (uint32_t j = 0; j < nf; j++) {
+					TokJob& t = feed.tj[idx[j]];
+					if (vp8g::make_desc(&t.kf, &t.hdr, filtered, mo, oo, &s.descs[j], false) != 0 ||
+					    vp8g::alloc_planes(&outs[idx[j]], t.kf.width, t.kf.height, false) != 0) {
+						feed.err[idx[j]] = errno ? errno : EINVAL;  // (cannot happen for a frame the header parse accepted)
+						s.descs[j].flags = 0;
+					}
+					s.jobs[j] = t.tf;
+					s.jobs[j].data = bo;
+					s.jobs[j].mb_offset = mo;
+					PTRY(hipMemcpyAsync(d + L.bits + bo, files[idx[j]].data + t.poff, t.psize, hipMemcpyHostToDevice, stream),
+					     "H2D");
+					mo += t.hdr.mb_total;
+					bo += bits_slot(t.psize);
+					oo = al256(oo + vp8g_i420_size(t.kf.width, t.kf.height));
+				}
+				PTRY(hipMemcpyAsync(d + L.jobs, s.jobs.data(), nf * sizeof(Vp8gTokFrame), hipMemcpyHostToDevice, stream), "H2D");
+			} else {
 				uint64_t mo = 0, vo = 0, oo = 0;
 				for (uint32_t j = 0; j < nf; j++) {
 					Vp8gPackedFrame& p = feed.pk[idx[j]];
@@ -313,14 +378,8 @@ VP8G_API int vp8g_decode_webp_batch(const ByteSpan* files, uint32_t n, int filte
 			PTRY(hipMemcpyAsync(d + L.desc, s.descs.data(), nf * sizeof(Vp8gFrameDesc), hipMemcpyHostToDevice, stream), "H2D");
 			PTRY(hipMemsetAsync(d + L.status, 0, 4, stream), "memset");
 			if (k > 1) PTRY(hipMemsetAsync(d + L.gprog, 0, (size_t)nf * k * 4, stream), "memset");
-			// -- expansion + recon(+LF)
+			// -- expansion (or device m05) + recon(+LF)
 			{
-				const uint64_t threads_x = mbs * 32;
-				hipLaunchKernelGGL(expand_kernel, dim3((uint32_t)((threads_x + 255) / 256)), dim3(256), 0, stream,
-				                   (const uint16_t*)(d + L.masks), (const uint32_t*)(d + L.mboff), (const int16_t*)(d + L.vals),
-				                   (uint32_t)mbs, (int16_t*)(d + L.cy), (int16_t*)(d + L.cu), (int16_t*)(d + L.cv),
-				                   (int16_t*)(d + L.cy2));
-				PTRY(hipGetLastError(), "expand launch");
 				Vp8gBatchArrays arr;
 				arr.coeff_y = (const int16_t*)(d + L.cy);
 				arr.coeff_u = (const int16_t*)(d + L.cu);
@@ -333,6 +392,22 @@ VP8G_API int vp8g_decode_webp_batch(const ByteSpan* files, uint32_t n, int filte
 				arr.bmode = d + L.bm;
 				arr.src = nullptr;
 				arr.status = (uint32_t*)(d + L.status);
+				if (tok) {
+					PTRY(hipMemsetAsync(d + L.cy, 0, L.cy2 + mbs * 32 - L.cy, stream), "memset");
+					if (vp8g_m05_batch_device(s.jobs.data(), (const Vp8gTokFrame*)(d + L.jobs), nf, d + L.bits, &arr, stream) != 0) {
+						he = hipGetLastError();
+						if (he == hipSuccess) he = hipErrorInvalidValue;
+						where = "m05 launch";
+						goto fail;
+					}
+				} else {
+					const uint64_t threads_x = mbs * 32;
+					hipLaunchKernelGGL(expand_kernel, dim3((uint32_t)((threads_x + 255) / 256)), dim3(256), 0, stream,
+					                   (const uint16_t*)(d + L.masks), (const uint32_t*)(d + L.mboff),
+					                   (const int16_t*)(d + L.vals), (uint32_t)mbs, (int16_t*)(d + L.cy), (int16_t*)(d + L.cu),
+					                   (int16_t*)(d + L.cv), (int16_t*)(d + L.cy2));
+					PTRY(hipGetLastError(), "expand launch");
+				}
 				PTRY(vp8g::launch_frames((const Vp8gFrameDesc*)(d + L.desc), nf, arr, d + L.out, max_cols, max_rows,
 				                         big ? d + L.gctx : nullptr, stream, nw, k, k > 1 ? d + L.mbox : nullptr,
 				                         k > 1 ? (uint32_t*)(d + L.gprog) : nullptr),
@@ -369,7 +444,7 @@ VP8G_API int vp8g_decode_webp_batch(const ByteSpan* files, uint32_t n, int filte
 	{
 		int first = 0;
 		for (uint32_t i = 0; i < n; i++) {
-			vp8f_packed_free(&feed.pk[i]);  // failed frames (the others were freed per chunk)
+			if (!tok) vp8f_packed_free(&feed.pk[i]);  // failed frames (the others were freed per chunk)
 			if (status) status[i] = feed.err[i];
 			if (feed.err[i] && !first) first = feed.err[i];
 			if (feed.err[i]) yuv420_free(&outs[i]);
@@ -392,11 +467,16 @@ fail:
 	}
 	if (stream) (void)hipStreamDestroy(stream);
 	for (uint32_t i = 0; i < n; i++) {
-		vp8f_packed_free(&feed.pk[i]);
+		if (!tok) vp8f_packed_free(&feed.pk[i]);
 		yuv420_free(&outs[i]);
 		if (status) status[i] = EIO;
 	}
 	errno = EIO;
 	return -1;
 #undef PTRY
+}
+
+VP8G_API int vp8g_decode_webp_batch(const ByteSpan* files, uint32_t n, int filtered, uint32_t threads, Yuv420Image* outs,
+                                    int* status) {
+	return vp8g_decode_webp_batch_ex(files, n, filtered, threads, 0, outs, status);
 }

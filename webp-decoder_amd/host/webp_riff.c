@@ -125,6 +125,36 @@ int vp8f_decode_packed_memory(const uint8_t* data, size_t size, Vp8gPackedFrame*
 	return rc;
 }
 
+int vp8f_token_header_memory(const uint8_t* data, size_t size, Vp8KeyFrameHeader* kf, Vp8DecodedFrame* hdr,
+                             Vp8gTokFrame* tf, uint64_t* payload_off, uint32_t* payload_size, int* stage) {
+	int st = 0, rc = -1;
+	WebPContainer c;
+	ByteSpan file = {data, size};
+	if (!kf || !hdr || !tf || !payload_off || !payload_size) {
+		errno = EINVAL;
+		st = 4;
+	} else if (webp_parse_simple_lossy(file, &c) != 0) {
+		st = 2;
+	} else if (c.vp8_chunk_size > 0xFFFFFFF0u) {
+		errno = EFBIG;
+		st = 4;
+	} else {
+		ByteSpan payload = {data + c.vp8_chunk_offset, c.vp8_chunk_size};
+		if (vp8_parse_keyframe_header(payload, kf) != 0 || !kf->is_key_frame) {
+			errno = EINVAL;
+			st = 3;
+		} else if (vp8f_token_header(payload, kf, hdr, tf) != 0) {
+			st = 4;
+		} else {
+			*payload_off = c.vp8_chunk_offset;
+			*payload_size = (uint32_t)c.vp8_chunk_size;
+			rc = 0;
+		}
+	}
+	if (stage) *stage = st;
+	return rc;
+}
+
 int vp8f_decode_file(const char* path, Vp8KeyFrameHeader* kf, Vp8DecodedFrame* out, int* stage) {
 	FILE* fp = fopen(path, "rb");
 	if (!fp) {

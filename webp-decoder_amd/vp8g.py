@@ -117,7 +117,18 @@ class Vp8gPackedFrame(C.Structure):
                 ("mb_off", C.POINTER(C.c_uint32)), ("values", C.POINTER(C.c_int16)), ("n_values", C.c_uint64)]
 
 
+class Vp8gTokFrame(C.Structure):
+    """include/vp8g.h: device m05 job of one frame (partition-0 bool state + token probabilities)."""
+    _fields_ = [("data", C.c_uint64), ("mb_offset", C.c_uint64), ("b_value", C.c_uint64), ("b_bits", C.c_int32),
+                ("b_range", C.c_uint32), ("b_next", C.c_uint32), ("p0_end", C.c_uint32), ("tok_off", C.c_uint32),
+                ("tok_end", C.c_uint32), ("mb_cols", C.c_uint32), ("mb_rows", C.c_uint32),
+                ("seg_enabled", C.c_uint8), ("seg_map_update", C.c_uint8), ("use_skip", C.c_uint8),
+                ("skip_prob", C.c_uint8), ("seg_probs", C.c_uint8 * 3), ("reserved", C.c_uint8),
+                ("coeff_probs", C.c_uint8 * (4 * 8 * 3 * 12))]
+
+
 PK_BLOCKS = 25  # per MB: Y 0..15, U 0..3, V 0..3, Y2
+VP8G_BATCH_DEVICE_M05 = 1
 VP8F_PACK_HASH = 1
 
 ENC_FORMATS = {"rgb": 0, "ppm": 1, "png": 2}
@@ -129,6 +140,7 @@ assert C.sizeof(Vp8CoeffStats) == 200
 assert C.sizeof(Vp8DecodedFrame) == 320
 assert C.sizeof(Yuv420Image) == 40
 assert C.sizeof(Vp8gFrameDesc) == 176
+assert C.sizeof(Vp8gTokFrame) == 1216
 
 VP8G_F_LOOPFILTER = 1
 VP8G_F_SIMPLE = 2
@@ -177,6 +189,9 @@ def host_lib():
         lib.vp8f_decode_packed_memory.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(Vp8gPackedFrame),
                                                   C.POINTER(C.c_int), C.c_uint]
         lib.vp8f_packed_free.argtypes = [C.POINTER(Vp8gPackedFrame)]
+        lib.vp8f_token_header_memory.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(Vp8KeyFrameHeader),
+                                                 C.POINTER(Vp8DecodedFrame), C.POINTER(Vp8gTokFrame),
+                                                 C.POINTER(C.c_uint64), C.POINTER(C.c_uint32), C.POINTER(C.c_int)]
         lib.vp8f_packed_free.restype = None
         lib._typed = True
     return lib
@@ -216,6 +231,10 @@ def gpu_lib():
                                                  C.c_void_p, C.c_void_p]
         lib.vp8g_decode_webp_batch.argtypes = [P(ByteSpan), C.c_uint32, C.c_int, C.c_uint32, P(Yuv420Image),
                                                P(C.c_int)]
+        lib.vp8g_decode_webp_batch_ex.argtypes = [P(ByteSpan), C.c_uint32, C.c_int, C.c_uint32, C.c_uint32,
+                                                  P(Yuv420Image), P(C.c_int)]
+        lib.vp8g_m05_batch_device.argtypes = [P(Vp8gTokFrame), C.c_void_p, C.c_uint32, C.c_void_p,
+                                              P(Vp8gBatchArrays), C.c_void_p]
         lib._typed = True
     return lib
 
@@ -330,15 +349,70 @@ def unpack_coeffs(pf: PackedFrame) -> dict:
             "coeff_v": dense[:, 20:24].reshape(-1), "coeff_y2": dense[:, 24].reshape(-1)}
 
 
-def gpu_decode_webp_batch(files: list[bytes], filtered: bool = True, threads: int = 0):
-    """vp8g_decode_webp_batch: .webp images -> (list of I420 bytes or None, list of errno)."""
+def token_header(data: bytes):
+    """vp8f_token_header_memory: (kf, hdr, Vp8gTokFrame, payload offset, payload size) or raises."""
+    lib = host_lib()
+    kf, hdr, tf = Vp8KeyFrameHeader(), Vp8DecodedFrame(), Vp8gTokFrame()
+    off, size, st = C.c_uint64(0), C.c_uint32(0), C.c_int(0)
+    buf = (C.c_uint8 * max(1, len(data))).from_buffer_copy(data or b"\0")
+    if lib.vp8f_token_header_memory(buf, len(data), C.byref(kf), C.byref(hdr), C.byref(tf), C.byref(off),
+                                    C.byref(size), C.byref(st)) != 0:
+        raise ValueError(f"vp8f_token_header_memory: stage {st.value}")
+    return kf, hdr, tf, off.value, size.value
+
+
+def gpu_m05(files: list[bytes]) -> list[dict]:
+    """vp8g_m05_batch_device over .webp images (one launch): per frame the m05 arrays as numpy,
+    named as FRAME_ARRAYS (skip_coeff excepted: the device does not keep it)."""
+    import torch
+    lib = gpu_lib()
+    hdrs = [token_header(b) for b in files]
+    n = len(files)
+    jobs = (Vp8gTokFrame * n)()
+    slots, mbs = [], []
+    bo = mo = 0
+    for i, (kf, hdr, tf, off, size) in enumerate(hdrs):
+        jobs[i] = tf
+        jobs[i].data, jobs[i].mb_offset = bo, mo
+        slots.append((bo, off, size))
+        mbs.append(hdr.mb_total)
+        bo += (size + 31) & ~15
+        mo += hdr.mb_total
+    bits = np.zeros(max(bo, 16), np.uint8)
+    for (b0, off, size), data in zip(slots, files):
+        bits[b0:b0 + size] = np.frombuffer(data, np.uint8, size, off)
+    dev = torch.device("cuda:0")
+    d_bits = torch.from_numpy(bits).to(dev)
+    d_jobs = torch.from_numpy(np.frombuffer(bytes(jobs), np.uint8).copy()).to(dev)
+    per = {n_: (dt, k) for n_, dt, k in FRAME_ARRAYS}
+    names = ["coeff_y", "coeff_u", "coeff_v", "coeff_y2", "ymode", "uv_mode", "segment_id", "has_coeff", "bmode"]
+    tdt = {np.dtype(np.int16): torch.int16, np.dtype(np.uint8): torch.uint8}
+    d = {k: torch.zeros(mo * per[k][1], dtype=tdt[np.dtype(per[k][0])], device=dev) for k in names}
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    arr = Vp8gBatchArrays(**{k: d[k].data_ptr() for k in names}, src=None, status=status.data_ptr())
+    torch.cuda.synchronize()
+    if lib.vp8g_m05_batch_device(jobs, d_jobs.data_ptr(), n, d_bits.data_ptr(), C.byref(arr), None) != 0:
+        raise RuntimeError(f"vp8g_m05_batch_device failed: {lib.vp8g_last_error()!r}")
+    torch.cuda.synchronize()
+    host = {k: v.cpu().numpy() for k, v in d.items()}
+    out, m0 = [], 0
+    for m in mbs:
+        out.append({k: host[k][m0 * per[k][1]:(m0 + m) * per[k][1]] for k in names})
+        m0 += m
+    return out
+
+
+def gpu_decode_webp_batch(files: list[bytes], filtered: bool = True, threads: int = 0, device_m05: bool = False):
+    """vp8g_decode_webp_batch(_ex): .webp images -> (list of I420 bytes or None, list of errno).
+    device_m05: m05 on the device (VP8G_BATCH_DEVICE_M05) instead of the host threads."""
     lib = gpu_lib()
     n = len(files)
     bufs = [(C.c_uint8 * max(1, len(b))).from_buffer_copy(b if b else b"\0") for b in files]
     spans = (ByteSpan * n)(*[ByteSpan(C.cast(bufs[i], C.POINTER(C.c_uint8)), len(files[i])) for i in range(n)])
     imgs = (Yuv420Image * n)()
     st = (C.c_int * n)()
-    rc = lib.vp8g_decode_webp_batch(spans, n, int(filtered), threads, imgs, st)
+    rc = lib.vp8g_decode_webp_batch_ex(spans, n, int(filtered), threads,
+                                       VP8G_BATCH_DEVICE_M05 if device_m05 else 0, imgs, st)
     if rc != 0 and all(s == 5 for s in st):  # EIO: device failure, nothing returned
         raise RuntimeError(f"vp8g_decode_webp_batch failed: {lib.vp8g_last_error()!r}")
     out = []
