@@ -67,6 +67,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     ap.add_argument("--e2e-frames", type=int, default=256,
                     help="frames of the end-to-end object (.webp bytes -> I420, vp8g_decode_webp_batch); 0 = off")
+    ap.add_argument("--e2e-device-frames", type=int, default=1024,
+                    help="frames of its device-m05 leg (VP8G_BATCH_DEVICE_M05: m05 on the device, one workgroup "
+                         "per frame, so it wants a large batch); 0 = off")
     ap.add_argument("--encode", default="png", choices=["none", "rgb", "ppm", "png"],
                     help="also time the m08/m09 stage on the batch's output (secondary object 'encode')")
     return ap.parse_args()
@@ -149,6 +152,28 @@ class EncodeStage:
     def file(self, i: int) -> bytes:
         o = self.outs[i]
         return self.out[o:o + self.file_len].cpu().numpy().tobytes()
+
+
+def end_to_end_device(manifest, n_frames, filtered, threads):
+    """The same path with m05 on the device: host threads parse only the
+    container and frame headers, the compressed payloads are uploaded, one workgroup per frame
+    decodes modes + tokens, then the recon(+LF) kernel and D2H as before."""
+    files = [(ROOT / "tests" / "fixtures" / r).read_bytes() for r in FIXTURES]
+    batch = [files[i % 4] for i in range(n_frames)]
+    vp8g.gpu_decode_webp_batch(batch[:8], filtered, threads, device_m05=True)  # warm
+    t = time.perf_counter()
+    outs, st = vp8g.gpu_decode_webp_batch(batch, filtered, threads, device_m05=True)
+    dt = time.perf_counter() - t
+    key = "yuvf_sha256" if filtered else "yuv_sha256"
+    ok = all(s == 0 for s in st) and all(hashlib.sha256(outs[i]).hexdigest() == manifest["files"][FIXTURES[i % 4]][key]
+                                         for i in range(n_frames))
+    del outs
+    return {"stage": "end to end with m05 on the device: .webp bytes in host memory -> I420 in host memory "
+                     "(container + frame header on host threads; payload upload, m05 (one workgroup per frame), "
+                     "recon+LF on the device; D2H)",
+            "value": round(n_frames * 3840 * 2160 / 1e6 / dt, 1), "unit": "MP/s", "frames": n_frames,
+            "threads": threads, "seconds": round(dt, 3),
+            "parity": f"bit-exact vs reference ({n_frames} frames sha256)" if ok else "MISMATCH"}
 
 
 def end_to_end(manifest, n_frames, filtered, threads):
@@ -318,6 +343,8 @@ def main():
     e2e = None
     if rank == 0 and world == 1 and args.e2e_frames > 0:
         e2e = end_to_end(manifest, args.e2e_frames, filtered, args.cpu_threads)
+        if args.e2e_device_frames > 0:
+            e2e["device_m05"] = end_to_end_device(manifest, args.e2e_device_frames, filtered, args.cpu_threads)
 
     stamp_shares = None
     if stamps:

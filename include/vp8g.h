@@ -260,9 +260,10 @@ int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int filtered, u
                               Yuv420Image* outs, int* status);
 
 /* Device m05 over n frames on `hip_stream`: h_jobs / d_jobs host and device copies of the jobs
- * (data = payload offset in d_bits, 4-aligned, with >= 8 readable bytes after the payload;
+ * (data = payload offset in d_bits, 4-aligned, with >= 512 readable bytes after the payload;
  * mb_offset = first MB in the arrays).  Writes ymode, uv_mode, segment_id, has_coeff, bmode and
- * the non-zero coefficients of `arrays` (the caller zeroes the four coefficient arrays first).
+ * the non-zero coefficients of `arrays` (the caller zeroes the four coefficient arrays first);
+ * arrays->status (required) gets VP8G_ERR_TIMEOUT if the two waves of a frame lose each other.
  * Asynchronous; 0 or -1 + errno (EINVAL for an inconsistent job, EIO on a launch failure). */
 int vp8g_m05_batch_device(const Vp8gTokFrame* h_jobs, const Vp8gTokFrame* d_jobs, uint32_t n, const uint8_t* d_bits,
                           const Vp8gBatchArrays* arrays, void* hip_stream);

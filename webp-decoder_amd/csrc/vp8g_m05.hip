@@ -4,12 +4,13 @@
 // VP8's arithmetic-coded partitions are serial chains (each bool's range depends on the previous
 // one), and a key frame with one token partition has exactly two of them: partition 0 (modes) and
 // the token partition.  There is no parallelism inside a frame, so the unit of parallelism is the
-// frame: one 64-thread workgroup decodes one frame with wave-uniform code.  Every value is the
-// same in all lanes (context words read from LDS go through readfirstlane), so the decoder state
-// lives in scalar registers, the bool decoder runs on the scalar ALU and the bitstream comes in
-// through scalar loads; lane 0 stores the results (vector stores only).  A batch of a few hundred
-// frames gives every CU one or more frames.  The two chains are interleaved MB by MB (modes of MB
-// m, then its tokens): they are independent streams read in the same raster order.
+// frame: one 64-thread workgroup decodes one frame with wave-uniform code.  Every value on the
+// decode chain is the same in all lanes, so the decoder state lives in scalar registers and the
+// bool decoder runs on the scalar ALU.  The chain is latency-bound, so nothing on it waits for
+// memory: the probability tables and a window of each partition sit in VGPR lanes and are read
+// with v_readlane (see "register tables" below).  A batch of a few hundred frames gives every CU
+// one or more frames.  The two chains are interleaved MB by MB (modes of MB m, then its tokens):
+// they are independent streams read in the same raster order.
 //
 // Semantics are those of the host front end (host/vp8_parse.c, itself pinned to the reference m05:
 // src/m05_tokens/vp8_tokens.c:275-352, :354-622, :868-926): de-zigzagged coefficients, explicit
@@ -66,35 +67,61 @@ enum { PLANE_Y_AFTER_Y2 = 0, PLANE_Y2 = 1, PLANE_UV = 2, PLANE_Y_ALONE = 3 };
 struct Out {
 	int16_t *cy, *cu, *cv, *cy2;
 	uint8_t *ymode, *uvmode, *seg, *hasc, *bmode;
+	uint32_t* status;  // VP8G_ERR_TIMEOUT if a ring wait gives up (never expected; keeps the grid finite)
 };
 
+// Register tables.  Every memory access on the serial chain is pure latency (a scalar-cache round
+// trip per token would dominate), so the tables consulted per token / per sub-block mode and the
+// bitstream itself are held in VGPR lanes -- loaded once per frame, or one window ahead -- and
+// read with v_readlane (lane index in an SGPR), a few cycles.
+DEV uint32_t lane() { return threadIdx.x & 63u; }
+DEV uint32_t rl(uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); }
+
 // RFC 6386 7 bool decoder in the host's formulation (host/vp8_bool.h): `value` holds the stream
-// bits, compared at `bits`.  Refilled 32 bits at a time; bytes at or past `end` read as zero (the
-// coder's padding), as in the host's byte-wise refill, so the compared values are identical.
+// bits, compared at `bits`.  Refilled 32 bits at a time from a 512-byte window of the partition
+// (two VGPRs of 64 big-endian dwords: `cur` at byte `base`, `nxt` after it, loaded one window
+// ahead); bytes at or past `end` read as zero (the coder's padding), as in the host's byte-wise
+// refill, so the compared values are identical.
 struct DBool {
 	uint64_t value;
 	int bits;
 	uint32_t range;
 	uint32_t next, end;
+	uint32_t base;       // window start (4-aligned)
+	uint32_t cur, nxt;   // per lane: dword base/4 + lane, big-endian (cur); + 64, as loaded (nxt)
 };
 
-// 4 big-endian stream bytes at payload offset pos (zero at and past end).  The payload starts
-// 4-aligned in the bitstream buffer and is followed by >= 8 readable bytes.
-DEV uint32_t be32_at(const uint8_t* pl, uint32_t pos, uint32_t end) {
-	if (pos >= end) return 0u;
-	const uint32_t al = pos & ~3u, sh = (pos & 3u) * 8u;
-	const uint32_t* w = (const uint32_t*)(pl + al);
-	const uint64_t x = ((uint64_t)w[1] << 32) | w[0];
-	uint32_t v = (uint32_t)(x >> sh);
-	const uint32_t n = end - pos;
-	if (n < 4u) v &= 0xFFFFFFFFu >> (32u - 8u * n);
-	return __builtin_bswap32(v);
+// The payload starts 4-B aligned in the bitstream buffer with >= 512 readable bytes after its end
+// (a window is loaded only while the read position is inside the partition), so the loads need no
+// guard (no exec-mask change on the chain); bytes past the end are masked in dfill.
+DEV uint32_t win_load(const uint8_t* pl, uint32_t at) { return *(const uint32_t*)(pl + at + 4u * lane()); }
+
+DEV void dinit(DBool& b, const uint8_t* pl, uint64_t value, int bits, uint32_t range, uint32_t next, uint32_t end) {
+	b.value = value, b.bits = bits, b.range = range, b.next = next, b.end = end;
+	b.base = next & ~3u;
+	b.cur = __builtin_bswap32(win_load(pl, b.base));
+	b.nxt = win_load(pl, b.base + 256u);
 }
 
 DEV void dfill(DBool& b, const uint8_t* pl) {
-	b.value = (b.value << 32) | be32_at(pl, b.next, b.end);
+	const uint32_t pos = b.next;
+	uint32_t v = 0;
+	if (pos < b.end) {
+		if (pos - b.base >= 256u) {  // slide the window (pos advances 4 bytes per refill)
+			b.cur = __builtin_bswap32(b.nxt);  // byte swap only now: the load has long landed
+			b.base += 256u;
+			b.nxt = win_load(pl, b.base + 256u);
+		}
+		const uint32_t idx = (pos - b.base) >> 2, s = (pos & 3u) * 8u;
+		const uint32_t hi = rl(b.cur, idx);
+		const uint32_t lo = idx < 63u ? rl(b.cur, idx + 1u) : __builtin_bswap32(rl(b.nxt, 0));
+		v = (uint32_t)(((((uint64_t)hi) << 32) | lo) >> (32u - s));
+		const uint32_t n = b.end - pos;
+		if (n < 4u) v &= 0xFFFFFFFFu << (32u - 8u * n);
+	}
+	b.value = (b.value << 32) | v;
 	b.bits += 32;
-	b.next += 4u;
+	b.next = pos + 4u;
 }
 
 DEV uint32_t dread(DBool& b, const uint8_t* pl, uint32_t prob) {
@@ -144,58 +171,72 @@ DEV uint32_t read_segment(DBool& b, const uint8_t* pl, uint32_t probs) {  // tre
 	return 2u + dread(b, pl, (probs >> 16) & 255u);
 }
 
-// DCT_CAT1..6 extra bits (RFC 6386 13.2): probabilities packed 4 per dword
-__constant__ uint32_t kCatProbs[6][3] = {
-	{159u, 0u, 0u},
-	{165u | 145u << 8, 0u, 0u},
-	{173u | 148u << 8 | 140u << 16, 0u, 0u},
-	{176u | 155u << 8 | 140u << 16 | 135u << 24, 0u, 0u},
-	{180u | 157u << 8 | 141u << 16 | 134u << 24, 130u, 0u},
-	{254u | 254u << 8 | 243u << 16 | 230u << 24, 196u | 177u << 8 | 153u << 16 | 140u << 24, 133u | 130u << 8 | 129u << 16},
-};
-DEV uint32_t read_cat(DBool& b, const uint8_t* pl, uint32_t cat) {
-	const uint32_t nbits = cat < 5u ? cat + 1u : 11u;
-	const uint32_t base = cat < 5u ? (3u + (2u << cat)) : 67u;  // 5 7 11 19 35 67
+// DCT_CAT1..6 magnitude: base + extra bits (RFC 6386 13.2), probabilities as immediates
+template <int N>
+DEV uint32_t read_bits(DBool& b, const uint8_t* pl, const uint8_t (&p)[N]) {
 	uint32_t e = 0;
-	for (uint32_t i = 0; i < nbits; i++) {
-		const uint32_t p = (kCatProbs[cat][i >> 2] >> (8u * (i & 3u))) & 255u;
-		e = 2u * e + dread(b, pl, p);
+#pragma unroll
+	for (int i = 0; i < N; i++) e = 2u * e + dread(b, pl, p[i]);
+	return e;
+}
+DEV uint32_t read_cat(DBool& b, const uint8_t* pl, uint32_t cat) {
+	constexpr uint8_t p1[1] = {159}, p2[2] = {165, 145}, p3[3] = {173, 148, 140}, p4[4] = {176, 155, 140, 135};
+	constexpr uint8_t p5[5] = {180, 157, 141, 134, 130};
+	constexpr uint8_t p6[11] = {254, 254, 243, 230, 196, 177, 153, 140, 133, 130, 129};
+	switch (cat) {
+		case 0: return 5u + read_bits(b, pl, p1);
+		case 1: return 7u + read_bits(b, pl, p2);
+		case 2: return 11u + read_bits(b, pl, p3);
+		case 3: return 19u + read_bits(b, pl, p4);
+		case 4: return 35u + read_bits(b, pl, p5);
+		default: return 67u + read_bits(b, pl, p6);
 	}
-	return base + e;
 }
 
+// Coefficient probabilities of one block type in lanes: `va` lane 2r + h = dword h (0, 1) of row r
+// (r = band * 3 + ctx, 24 rows), `vb` lane r + vo = dword 2.
+struct TypeTab {
+	uint32_t va, vb, vo;
+};
+
 // One 4x4 block's tokens (RFC 6386 13; host/vp8_parse.c read_block): the non-zero values go to
-// dst[natural position] (lane 0 stores); returns whether any value is non-zero.  `probs` points at
-// the [8][3] rows of the block type (12 bytes each).
-DEV bool read_block(DBool& b, const uint8_t* pl, const uint32_t* probs, uint32_t first, uint32_t ctx, int16_t* dst,
-                    bool l0) {
+// dst[natural position]; returns whether any value is non-zero.  Every lane stores the same value
+// to the same address (no exec-mask juggling on the serial path).
+DEV bool read_block(DBool& b, const uint8_t* pl, const TypeTab& t, uint32_t first, uint32_t ctx, int16_t* dst) {
 	bool nz = false;
 	uint32_t pos = first;
 	uint32_t ri = nib(kBand4, pos) * 3u + ctx;
 	bool skip_eob = false;
 	while (true) {
-		const Row p{probs[ri * 3u], probs[ri * 3u + 1u], probs[ri * 3u + 2u]};
-		if (!skip_eob && !dread(b, pl, pb(p, 0))) break;  // EOB
-		if (!dread(b, pl, pb(p, 1))) {                     // DCT_0: the next token has no EOB branch
+		const uint32_t w0 = rl(t.va, 2u * ri);
+		if (!skip_eob && !dread(b, pl, w0 & 255u)) break;  // EOB
+		if (!dread(b, pl, (w0 >> 8) & 255u)) {                 // DCT_0: the next token has no EOB branch
 			if (++pos == 16u) break;
 			ri = nib(kBand4, pos) * 3u;
 			skip_eob = true;
 			continue;
 		}
 		uint32_t mag;
-		if (!dread(b, pl, pb(p, 2))) {
+		if (!dread(b, pl, (w0 >> 16) & 255u)) {
 			mag = 1u;
-		} else if (!dread(b, pl, pb(p, 3))) {
-			mag = dread(b, pl, pb(p, 4)) ? 3u + dread(b, pl, pb(p, 5)) : 2u;
 		} else {
-			uint32_t cat;
-			if (!dread(b, pl, pb(p, 6))) cat = dread(b, pl, pb(p, 7));
-			else if (!dread(b, pl, pb(p, 8))) cat = 2u + dread(b, pl, pb(p, 9));
-			else cat = 4u + dread(b, pl, pb(p, 10));
-			mag = read_cat(b, pl, cat);
+			const uint32_t w1 = rl(t.va, 2u * ri + 1u);
+			if (!dread(b, pl, w0 >> 24)) {
+				mag = dread(b, pl, w1 & 255u) ? 3u + dread(b, pl, (w1 >> 8) & 255u) : 2u;
+			} else {
+				uint32_t cat;
+				if (!dread(b, pl, (w1 >> 16) & 255u)) {
+					cat = dread(b, pl, w1 >> 24);
+				} else {
+					const uint32_t w2 = rl(t.vb, ri + t.vo);
+					if (!dread(b, pl, w2 & 255u)) cat = 2u + dread(b, pl, (w2 >> 8) & 255u);
+					else cat = 4u + dread(b, pl, (w2 >> 16) & 255u);
+				}
+				mag = read_cat(b, pl, cat);
+			}
 		}
 		const uint32_t neg = dread(b, pl, 128);
-		if (l0) dst[nib(kScan4, pos)] = (int16_t)(neg ? -(int)mag : (int)mag);
+		dst[nib(kScan4, pos)] = (int16_t)(neg ? -(int)mag : (int)mag);
 		nz = true;
 		if (++pos == 16u) break;
 		ri = nib(kBand4, pos) * 3u + (mag == 1u ? 1u : 2u);
@@ -204,33 +245,51 @@ DEV bool read_block(DBool& b, const uint8_t* pl, const uint32_t* probs, uint32_t
 	return nz;
 }
 
-// Per MB column in LDS, one dword: bits 0..8 token contexts (Y 0..3, U 4..5, V 6..7, Y2 8),
-// bits 16..31 the bottom row's sub-block modes (4 nibbles; B_DC = 0 above the frame).
-__global__ __launch_bounds__(64) void m05_kernel(const Vp8gTokFrame* __restrict__ jobs, const uint8_t* __restrict__ bits,
-                                                 Out o) {
-	extern __shared__ uint32_t above[];
-	const Vp8gTokFrame& J = jobs[blockIdx.x];
-	const uint32_t cols = J.mb_cols, rows = J.mb_rows;
-	const bool l0 = threadIdx.x == 0;
-	for (uint32_t i = threadIdx.x; i < cols; i += 64u) above[i] = 0;
-	__syncthreads();
-	const uint8_t* pl = bits + J.data;
+// Per-frame workgroup of two waves, one per partition (their chains are independent):
+//   wave 0 ("modes") decodes partition 0 -- segment, skip flag, luma / chroma / sub-block modes --
+//          writes the mode arrays and, per MB, a flag byte (skip, has Y2) into an LDS ring;
+//   wave 1 ("tokens") decodes the token partition MB by MB as the ring fills.
+// The token chain is the long one; taking the modes off it shortens the frame's critical path.
+// Ring protocol (LDS only, one writer per word): the modes wave writes ring[m] and then
+// prod = m + 1; the tokens wave reads prod, then ring[m]; it publishes cons every 64 MBs and the
+// modes wave stays less than kRing MBs ahead of it.  LDS operations of a wave complete in order,
+// so volatile accesses (no compiler reordering) are enough; s_sleep while waiting.
+constexpr uint32_t kRing = 1024;
+constexpr uint32_t kMaxPolls = 1u << 24;  // a few seconds of s_sleep
+// LDS pointers typed as such: a volatile generic pointer would become flat accesses, whose
+// completion the compiler tracks with vmcnt (so every poll would also wait for the wave's stores)
+typedef __attribute__((address_space(3))) volatile uint32_t lds_u32;
+typedef __attribute__((address_space(3))) volatile uint8_t lds_u8;
+
+DEV void modes_wave(const Vp8gTokFrame& J, const uint8_t* pl, Out o, lds_u32* ctl, lds_u8* ring, lds_u32* above_b) {
+	const uint32_t L = lane(), cols = J.mb_cols, rows = J.mb_rows;
+	uint32_t bl[3], bh[3];  // sub-block mode rows 0..63 / 64..99 in lanes
+#pragma unroll
+	for (int x = 0; x < 3; x++) {
+		bl[x] = kBmodeProbs.w[L][x];
+		bh[x] = L < 36u ? kBmodeProbs.w[64u + L][x] : 0u;
+	}
 	const uint32_t flags = *(const uint32_t*)&J.seg_enabled;  // seg_enabled | seg_map_update | use_skip | skip_prob
 	const bool seg_map = (flags & 0xFFu) && ((flags >> 8) & 0xFFu);
 	const bool use_skip = (flags >> 16) & 0xFFu;
 	const uint32_t skip_prob = flags >> 24;
 	const uint32_t seg_probs = *(const uint32_t*)J.seg_probs;
-	const uint32_t* const cprobs = (const uint32_t*)J.coeff_probs;  // [4][8][3] rows of 3 dwords
-	DBool hb{J.b_value, J.b_bits, J.b_range, J.b_next, J.p0_end};
-	DBool tb{0, -8, 255u, J.tok_off, J.tok_end};
-	dfill(tb, pl);
+	DBool hb;
+	dinit(hb, pl, J.b_value, J.b_bits, J.b_range, J.b_next, J.p0_end);
+	uint32_t m = 0, cons = 0;
 	for (uint32_t r = 0; r < rows; r++) {
-		uint32_t left = 0;    // token contexts, bits as in above[]
 		uint32_t left_b = 0;  // right column's sub-block modes, 4 nibbles
-		for (uint32_t c = 0; c < cols; c++) {
-			const uint64_t mb = J.mb_offset + (uint64_t)r * cols + c;
-			uint32_t ab = __builtin_amdgcn_readfirstlane(above[c]);
-			// ---- modes (partition 0; RFC 6386 11, 19.3)
+		for (uint32_t c = 0; c < cols; c++, m++) {
+			for (uint32_t polls = 0; m - cons >= kRing; polls++) {
+				if (polls == kMaxPolls) {
+					if (L == 0) atomicOr(o.status, VP8G_ERR_TIMEOUT);
+					break;
+				}
+				__builtin_amdgcn_s_sleep(2);
+				cons = __builtin_amdgcn_readfirstlane(ctl[1]);
+			}
+			const uint64_t mb = J.mb_offset + m;
+			const uint32_t ab = __builtin_amdgcn_readfirstlane(above_b[c]);
 			const uint32_t seg = seg_map ? read_segment(hb, pl, seg_probs) : 0u;
 			const uint32_t skip = use_skip ? dread(hb, pl, skip_prob) : 0u;
 			const uint32_t ym = read_ymode(hb, pl);
@@ -239,24 +298,71 @@ __global__ __launch_bounds__(64) void m05_kernel(const Vp8gTokFrame* __restrict_
 				bm = 0;
 				for (uint32_t i = 0; i < 16u; i++) {
 					const uint32_t y = i >> 2, x = i & 3u;
-					const uint32_t a = y ? nib(bm, i - 4u) : (ab >> (16u + 4u * x)) & 15u;
+					const uint32_t a = y ? nib(bm, i - 4u) : (ab >> (4u * x)) & 15u;
 					const uint32_t l = x ? nib(bm, i - 1u) : (left_b >> (4u * y)) & 15u;
-					const uint32_t* w = kBmodeProbs.w[a * 10u + l];
-					bm |= (uint64_t)read_bmode(hb, pl, Row{w[0], w[1], w[2]}) << (4u * i);
+					const uint32_t ri = a * 10u + l;
+					const Row p = ri < 64u ? Row{rl(bl[0], ri), rl(bl[1], ri), rl(bl[2], ri)}
+					                       : Row{rl(bh[0], ri - 64u), rl(bh[1], ri - 64u), rl(bh[2], ri - 64u)};
+					bm |= (uint64_t)read_bmode(hb, pl, p) << (4u * i);
 				}
 			} else {
 				// implied sub-block context: DC->B_DC, V->B_VE, H->B_HE, TM->B_TM
 				const uint32_t im = (0x1320u >> (4u * ym)) & 15u;
 				bm = (uint64_t)im * 0x1111111111111111ull;
 			}
-			const uint32_t bottom = (uint32_t)(bm >> 48) & 0xFFFFu;
 			left_b = 0;
 			for (uint32_t y = 0; y < 4u; y++) left_b |= nib(bm, 4u * y + 3u) << (4u * y);
 			const uint32_t uvm = read_uvmode(hb, pl);
-			// ---- tokens (token partition; RFC 6386 13)
-			const bool has_y2 = ym != 4u;
+			if (L == 0) {
+				above_b[c] = (uint32_t)(bm >> 48) & 0xFFFFu;
+				ring[m & (kRing - 1u)] = (uint8_t)(skip | (ym != 4u ? 2u : 0u));
+				ctl[0] = m + 1u;
+			}
+			o.seg[mb] = (uint8_t)seg;
+			o.ymode[mb] = (uint8_t)ym;
+			o.uvmode[mb] = (uint8_t)uvm;
+			uint32_t bw[4];
+			for (int i = 0; i < 4; i++) {
+				const uint32_t q = (uint32_t)(bm >> (16 * i));
+				bw[i] = (q & 15u) | ((q >> 4) & 15u) << 8 | ((q >> 8) & 15u) << 16 | ((q >> 12) & 15u) << 24;
+			}
+			if (L == 0) *(uint4*)(o.bmode + mb * 16u) = make_uint4(bw[0], bw[1], bw[2], bw[3]);
+		}
+	}
+}
+
+DEV void tokens_wave(const Vp8gTokFrame& J, const uint8_t* pl, Out o, lds_u32* ctl, lds_u8* ring, lds_u32* above) {
+	const uint32_t L = lane(), cols = J.mb_cols, rows = J.mb_rows;
+	// coefficient rows of the 4 block types in lanes (TypeTab)
+	const uint32_t* const cp = (const uint32_t*)J.coeff_probs;  // [4][24] rows of 3 dwords
+	uint32_t va[4];
+#pragma unroll
+	for (int t = 0; t < 4; t++) va[t] = L < 48u ? cp[t * 72 + (L >> 1) * 3 + (L & 1u)] : 0u;
+	uint32_t vb[2];
+#pragma unroll
+	for (int k = 0; k < 2; k++) vb[k] = (L & 31u) < 24u ? cp[(2 * k + (L >> 5)) * 72 + (L & 31u) * 3 + 2] : 0u;
+	DBool tb;
+	dinit(tb, pl, 0, -8, 255u, J.tok_off, J.tok_end);
+	dfill(tb, pl);
+	uint32_t m = 0, prod = 0;
+	for (uint32_t r = 0; r < rows; r++) {
+		uint32_t left = 0;  // token contexts, bits as in above[]
+		for (uint32_t c = 0; c < cols; c++, m++) {
+			for (uint32_t polls = 0; m >= prod; polls++) {
+				if (polls == kMaxPolls) {
+					if (L == 0) atomicOr(o.status, VP8G_ERR_TIMEOUT);
+					prod = m + 1u;
+					break;
+				}
+				prod = __builtin_amdgcn_readfirstlane(ctl[0]);
+				if (m >= prod) __builtin_amdgcn_s_sleep(1);
+			}
+			const uint32_t fl = __builtin_amdgcn_readfirstlane(ring[m & (kRing - 1u)]);
+			const uint64_t mb = J.mb_offset + m;
+			uint32_t ab = __builtin_amdgcn_readfirstlane(above[c]);
+			const bool has_y2 = (fl & 2u) != 0;
 			bool any = false;
-			if (skip) {
+			if (fl & 1u) {
 				// no tokens: the contexts of the MB's blocks become 0; Y2's only if the MB has one
 				const uint32_t clr = has_y2 ? 0x1FFu : 0xFFu;
 				left &= ~clr;
@@ -278,36 +384,48 @@ __global__ __launch_bounds__(64) void m05_kernel(const Vp8gTokFrame* __restrict_
 						li = 4u + 2u * p + (jj >> 1), ai = 4u + 2u * p + (jj & 1u);
 						dst = (p ? o.cv : o.cu) + (mb * 4u + jj) * 16u;
 					}
+					const TypeTab tt{type == 0 ? va[0] : type == 1 ? va[1] : type == 2 ? va[2] : va[3],
+					                 type < 2 ? vb[0] : vb[1], (type & 1u) * 32u};
 					const uint32_t ctx = ((left >> li) & 1u) + ((ab >> ai) & 1u);
-					const bool nz = read_block(tb, pl, cprobs + type * 72u, first, ctx, dst, l0);
+					const bool nz = read_block(tb, pl, tt, first, ctx, dst);
 					any |= nz;
 					left = (left & ~(1u << li)) | ((uint32_t)nz << li);
 					ab = (ab & ~(1u << ai)) | ((uint32_t)nz << ai);
 				}
 			}
-			ab = (ab & 0xFFFFu) | (bottom << 16);
-			if (l0) {
+			if (L == 0) {
 				above[c] = ab;
-				o.seg[mb] = (uint8_t)seg;
-				o.ymode[mb] = (uint8_t)ym;
-				o.uvmode[mb] = (uint8_t)uvm;
-				o.hasc[mb] = (uint8_t)any;
-				uint32_t bw[4];
-				for (int i = 0; i < 4; i++) {
-					const uint32_t q = (uint32_t)(bm >> (16 * i));
-					bw[i] = (q & 15u) | ((q >> 4) & 15u) << 8 | ((q >> 8) & 15u) << 16 | ((q >> 12) & 15u) << 24;
-				}
-				*(uint4*)(o.bmode + mb * 16u) = make_uint4(bw[0], bw[1], bw[2], bw[3]);
+				if ((m & 63u) == 63u) ctl[1] = m + 1u;
 			}
+			o.hasc[mb] = (uint8_t)any;
 		}
 	}
+}
+
+// LDS: ctl[2] (prod, cons), ring[kRing] flag bytes, then per MB column the token contexts
+// (bits 0..8: Y 0..3, U 4..5, V 6..7, Y2 8) and the bottom row's sub-block modes (4 nibbles;
+// B_DC = 0 above the frame).
+__global__ __launch_bounds__(128) void m05_kernel(const Vp8gTokFrame* __restrict__ jobs, const uint8_t* __restrict__ bits,
+                                                  Out o) {
+	extern __shared__ uint32_t sm[];
+	const Vp8gTokFrame& J = jobs[blockIdx.x];
+	const uint32_t cols = J.mb_cols;
+	const uint32_t words = 2u + kRing / 4u + 2u * cols;
+	for (uint32_t i = threadIdx.x; i < words; i += 128u) sm[i] = 0;
+	__syncthreads();
+	lds_u32* const ctl = (lds_u32*)sm;
+	lds_u8* const ring = (lds_u8*)(sm + 2);
+	lds_u32* const above = (lds_u32*)(sm + 2 + kRing / 4u);
+	const uint8_t* pl = bits + J.data;
+	if ((__builtin_amdgcn_readfirstlane(threadIdx.x) >> 6) == 0) modes_wave(J, pl, o, ctl, ring, above + cols);
+	else tokens_wave(J, pl, o, ctl, ring, above);
 }
 
 }  // namespace
 
 VP8G_API int vp8g_m05_batch_device(const Vp8gTokFrame* h_jobs, const Vp8gTokFrame* d_jobs, uint32_t n,
                                    const uint8_t* d_bits, const Vp8gBatchArrays* arrays, void* hip_stream) {
-	if (!h_jobs || !d_jobs || !d_bits || !arrays || n == 0) {
+	if (!h_jobs || !d_jobs || !d_bits || !arrays || !arrays->status || n == 0) {
 		errno = EINVAL;
 		return -1;
 	}
@@ -332,7 +450,9 @@ VP8G_API int vp8g_m05_batch_device(const Vp8gTokFrame* h_jobs, const Vp8gTokFram
 	o.seg = const_cast<uint8_t*>(arrays->segment_id);
 	o.hasc = const_cast<uint8_t*>(arrays->has_coeff);
 	o.bmode = const_cast<uint8_t*>(arrays->bmode);
-	hipLaunchKernelGGL(m05_kernel, dim3(n), dim3(64), max_cols * 4u, (hipStream_t)hip_stream, d_jobs, d_bits, o);
+	o.status = arrays->status;
+	hipLaunchKernelGGL(m05_kernel, dim3(n), dim3(128), (2u + kRing / 4u + 2u * max_cols) * 4u, (hipStream_t)hip_stream,
+	                   d_jobs, d_bits, o);
 	const hipError_t e = hipGetLastError();
 	if (e != hipSuccess) {
 		vp8g::set_error_text("m05 launch", e);

@@ -83,9 +83,9 @@ __global__ __launch_bounds__(256) void expand_kernel(const uint16_t* __restrict_
 }
 
 inline uint64_t al256(uint64_t x) { return (x + 255u) & ~(uint64_t)255u; }
-// bitstream slot of a payload: 16-B aligned start, >= 16 bytes of slack (the device bool
-// decoder reads whole aligned dwords up to 8 bytes past a partition's end)
-inline uint64_t bits_slot(uint32_t psize) { return ((uint64_t)psize + 16u + 15u) & ~(uint64_t)15u; }
+// bitstream slot of a payload: 16-B aligned start, >= 512 bytes of slack (the device bool
+// decoder loads its 256-byte windows one ahead, up to 512 bytes past a partition's end)
+inline uint64_t bits_slot(uint32_t psize) { return ((uint64_t)psize + 512u + 15u) & ~(uint64_t)15u; }
 
 // Host half of a device-m05 frame.
 struct TokJob {

@@ -376,7 +376,7 @@ def gpu_m05(files: list[bytes]) -> list[dict]:
         jobs[i].data, jobs[i].mb_offset = bo, mo
         slots.append((bo, off, size))
         mbs.append(hdr.mb_total)
-        bo += (size + 31) & ~15
+        bo += (size + 512 + 15) & ~15  # >= 512 readable bytes after each payload
         mo += hdr.mb_total
     bits = np.zeros(max(bo, 16), np.uint8)
     for (b0, off, size), data in zip(slots, files):
@@ -394,6 +394,8 @@ def gpu_m05(files: list[bytes]) -> list[dict]:
     if lib.vp8g_m05_batch_device(jobs, d_jobs.data_ptr(), n, d_bits.data_ptr(), C.byref(arr), None) != 0:
         raise RuntimeError(f"vp8g_m05_batch_device failed: {lib.vp8g_last_error()!r}")
     torch.cuda.synchronize()
+    if int(status.item()) != 0:
+        raise RuntimeError(f"vp8g_m05_batch_device: device status {int(status.item())}")
     host = {k: v.cpu().numpy() for k, v in d.items()}
     out, m0 = [], 0
     for m in mbs:
