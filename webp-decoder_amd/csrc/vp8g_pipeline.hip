@@ -38,10 +38,11 @@ namespace {
 
 constexpr uint32_t kChunkFrames = 64;          // frames per device chunk (at most)
 constexpr uint64_t kChunkMbs = 2u << 20;       // macroblocks per chunk (at most, unless one frame is bigger)
-// device m05: one wavefront per frame, so a chunk wants many frames (~830 B of device buffers
-// per MB: 16M MBs ~ 13 GB per slot, two slots)
+// device m05: one workgroup per frame and a chunk's m05 time is its slowest frame's, so a chunk
+// wants as many frames as the chip runs at once (~1500 at full scalar-unit load): 1024 4K frames,
+// ~1.2 KB of device buffers per MB (coefficients, side arrays, I420 out) = ~41 GB per slot
 constexpr uint32_t kTokChunkFrames = 1024;
-constexpr uint64_t kTokChunkMbs = 16u << 20;
+constexpr uint64_t kTokChunkMbs = 34u << 20;
 constexpr uint32_t kNb = VP8G_PK_BLOCKS;
 
 // Packed -> dense coefficients.  32 lanes per MB; lane b < 25 owns block b (Y 0..15, U 0..3,
@@ -170,7 +171,8 @@ struct Feed {
 struct Slot {
 	uint8_t* buf = nullptr;
 	size_t cap = 0;
-	hipEvent_t done = nullptr;
+	hipEvent_t done = nullptr;     // the chunk's D2H finished (copy stream)
+	hipEvent_t kdone = nullptr;    // the chunk's kernels finished (compute stream)
 	bool busy = false;
 	std::vector<uint32_t> frames;  // frame indices of the chunk (packed data freed when the slot is reused)
 	std::vector<Vp8gFrameDesc> descs;
@@ -227,7 +229,8 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 	pool.reserve(threads);
 	for (uint32_t t = 0; t < threads; t++) pool.emplace_back([&feed] { feed.work(); });
 
-	hipStream_t stream = nullptr;
+	hipStream_t stream = nullptr;  // uploads and kernels
+	hipStream_t copy = nullptr;    // downloads: chunk k's D2H overlaps chunk k+1's kernels
 	Slot slots[2];
 	uint32_t released = 0;  // frames whose packed data is freed (all below this index)
 	const char* where = nullptr;
@@ -264,7 +267,11 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 	} while (0)
 
 	PTRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "stream");
-	for (Slot& s : slots) PTRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), "event");
+	PTRY(hipStreamCreateWithFlags(&copy, hipStreamNonBlocking), "stream");
+	for (Slot& s : slots) {
+		PTRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), "event");
+		PTRY(hipEventCreateWithFlags(&s.kdone, hipEventDisableTiming), "event");
+	}
 
 	{
 		uint32_t a = 0, chunk = 0;
@@ -413,18 +420,20 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 				                         k > 1 ? (uint32_t*)(d + L.gprog) : nullptr),
 				     "recon launch");
 			}
-			// -- D2H into the callers' images
+			// -- D2H into the callers' images, on the copy stream once the kernels are done
+			PTRY(hipEventRecord(s.kdone, stream), "event");
+			PTRY(hipStreamWaitEvent(copy, s.kdone, 0), "event");
 			for (uint32_t j = 0; j < nf; j++) {
 				const Vp8gFrameDesc& fd = s.descs[j];
 				Yuv420Image& img = outs[idx[j]];
 				if (!img.y) continue;
 				const size_t ysz = (size_t)fd.stride_y * fd.height, uvsz = (size_t)fd.stride_uv * ((fd.height + 1) / 2);
-				PTRY(hipMemcpyAsync(img.y, d + L.out + fd.out_y, ysz, hipMemcpyDeviceToHost, stream), "D2H");
-				PTRY(hipMemcpyAsync(img.u, d + L.out + fd.out_u, uvsz, hipMemcpyDeviceToHost, stream), "D2H");
-				PTRY(hipMemcpyAsync(img.v, d + L.out + fd.out_v, uvsz, hipMemcpyDeviceToHost, stream), "D2H");
+				PTRY(hipMemcpyAsync(img.y, d + L.out + fd.out_y, ysz, hipMemcpyDeviceToHost, copy), "D2H");
+				PTRY(hipMemcpyAsync(img.u, d + L.out + fd.out_u, uvsz, hipMemcpyDeviceToHost, copy), "D2H");
+				PTRY(hipMemcpyAsync(img.v, d + L.out + fd.out_v, uvsz, hipMemcpyDeviceToHost, copy), "D2H");
 			}
-			PTRY(hipMemcpyAsync(&s.status, d + L.status, 4, hipMemcpyDeviceToHost, stream), "D2H");
-			PTRY(hipEventRecord(s.done, stream), "event");
+			PTRY(hipMemcpyAsync(&s.status, d + L.status, 4, hipMemcpyDeviceToHost, copy), "D2H");
+			PTRY(hipEventRecord(s.done, copy), "event");
 			s.busy = true;
 			released = b;
 			feed.set_limit(released + window);
@@ -438,9 +447,11 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 	pool.clear();
 	for (Slot& s : slots) {
 		if (s.done) (void)hipEventDestroy(s.done);
+		if (s.kdone) (void)hipEventDestroy(s.kdone);
 		if (s.buf) (void)hipFree(s.buf);
 	}
 	(void)hipStreamDestroy(stream);
+	(void)hipStreamDestroy(copy);
 	{
 		int first = 0;
 		for (uint32_t i = 0; i < n; i++) {
@@ -460,12 +471,15 @@ fail:
 	feed.stop();
 	for (auto& t : pool) t.join();
 	if (stream) (void)hipStreamSynchronize(stream);
+	if (copy) (void)hipStreamSynchronize(copy);
 	vp8g::set_error_text(where ? where : "pipeline", he);
 	for (Slot& s : slots) {
 		if (s.done) (void)hipEventDestroy(s.done);
+		if (s.kdone) (void)hipEventDestroy(s.kdone);
 		if (s.buf) (void)hipFree(s.buf);
 	}
 	if (stream) (void)hipStreamDestroy(stream);
+	if (copy) (void)hipStreamDestroy(copy);
 	for (uint32_t i = 0; i < n; i++) {
 		if (!tok) vp8f_packed_free(&feed.pk[i]);
 		yuv420_free(&outs[i]);
