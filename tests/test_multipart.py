@@ -1,0 +1,59 @@
+"""multi-partition token streams (RFC 6386 9.5; the reference rejects them,
+vp8_tokens.c:357-360, and its corpus holds none -- parity unpinned against the reference).
+
+Fixtures are generated from the corpus by re-encoding each frame's decisions with its tokens
+spread over 2 / 4 / 8 partitions (tests/multipart.py, oracle/vp8_repartition.c), so the expected
+result is the original frame's: same m05 output, same pixels (whose sha256 the reference
+decoder produced, tests/golden/manifest.json).  The generator itself is pinned by the 1-partition
+re-encode reproducing the original m05 arrays exactly."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from conftest import FIXTURES
+from multipart import repartition
+
+SIDE = ("ymode", "uv_mode", "segment_id", "has_coeff", "bmode")
+
+
+def dense(vp8g, data):
+    kf, df, st = vp8g.Vp8KeyFrameHeader(), vp8g.Vp8DecodedFrame(), C.c_int(0)
+    buf = (C.c_uint8 * len(data)).from_buffer_copy(data)
+    rc = vp8g.host_lib().vp8f_decode_memory(buf, len(data), C.byref(kf), C.byref(df), C.byref(st))
+    if rc != 0:
+        return None
+    f = vp8g.Frame(kf, df)
+    out = {k: f.array(k).copy() for k, _, _ in vp8g.FRAME_ARRAYS}
+    f.free()
+    return out
+
+
+def test_generator_one_partition_round_trip(vp8g, manifest):
+    for rel in sorted(manifest["files"])[::6]:
+        data = (FIXTURES / rel).read_bytes()
+        a, b = dense(vp8g, data), dense(vp8g, repartition(data, 0))
+        assert all(np.array_equal(a[k], b[k]) for k in a), rel
+
+
+@pytest.mark.parametrize("log2k", [1, 2, 3])
+def test_host_multi_partition_equals_original(vp8g, manifest, log2k):
+    for rel in sorted(manifest["files"])[::5]:
+        data = (FIXTURES / rel).read_bytes()
+        m = repartition(data, log2k)
+        assert dense(vp8g, m) is None  # the reference-equivalent front end: ENOTSUP
+        with pytest.raises(ValueError):
+            vp8g.PackedFrame(m)  # opt-in only
+        p0, p1 = vp8g.PackedFrame(data), vp8g.PackedFrame(m, multi_partition=True)
+        assert np.array_equal(p0.masks(), p1.masks()) and np.array_equal(p0.values(), p1.values()), rel
+        assert all(np.array_equal(p0.side(k), p1.side(k)) for k in SIDE), rel
+
+
+def test_partition_table_rejects_overruns(vp8g, manifest):
+    data = (FIXTURES / sorted(manifest["files"])[3]).read_bytes()
+    m = bytearray(repartition(data, 2))
+    tag = m[20] | m[21] << 8 | m[22] << 16
+    fpl = tag >> 5
+    m[20 + 10 + fpl:20 + 10 + fpl + 3] = b"\xff\xff\xff"  # first partition size past the end
+    with pytest.raises(ValueError):
+        vp8g.PackedFrame(bytes(m), multi_partition=True)

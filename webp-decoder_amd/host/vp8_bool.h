@@ -17,7 +17,21 @@
 #include <stddef.h>
 #include <stdint.h>
 
-typedef struct {
+typedef struct Vp8Bool Vp8Bool;
+
+/* Test-only trace hooks (oracle/vp8_repartition.c builds the front end with VP8_BOOL_TRACE to
+ * record every decoded (probability, bit) and re-encode streams); no-ops in the product. */
+#ifdef VP8_BOOL_TRACE
+void vp8_trace_bool(const Vp8Bool* b, uint32_t prob, int bit);
+void vp8_trace_mark(int what, uint32_t arg);
+#define VP8B_TRACE(b, prob, bit) vp8_trace_bool(b, prob, bit)
+#define VP8_TRACE_MARK(what, arg) vp8_trace_mark(what, arg)
+#else
+#define VP8B_TRACE(b, prob, bit) ((void)0)
+#define VP8_TRACE_MARK(what, arg) ((void)0)
+#endif
+
+struct Vp8Bool {
 	const uint8_t* next; /* next unread byte */
 	const uint8_t* end;
 	uint64_t value;
@@ -25,7 +39,7 @@ typedef struct {
 	uint32_t range;  /* 128..255 between calls */
 	uint64_t shifts; /* total normalisation shifts so far */
 	size_t size;     /* partition size in bytes */
-} Vp8Bool;
+};
 
 static inline void vp8b_fill(Vp8Bool* b) {
 	while (b->bits <= 48) {
@@ -65,6 +79,7 @@ static inline int vp8b_read(Vp8Bool* b, uint32_t prob) {
 	b->bits -= sh;
 	b->shifts += (uint64_t)sh;
 	if (b->bits < 0) vp8b_fill(b);
+	VP8B_TRACE(b, prob, bit);
 	return bit;
 }
 

@@ -47,10 +47,17 @@ int vp8f_decode_memory(const uint8_t* data, size_t size, Vp8KeyFrameHeader* kf, 
  * non-zero mask and values (no dense coefficient arrays).  The FNV coefficient hash is computed
  * only with VP8F_PACK_HASH (stats.coeff_hash_fnv1a64 = 0 otherwise).  Reentrant. */
 #define VP8F_PACK_HASH 1u
+/* also accept 2/4/8 token partitions (RFC 6386 9.5), which the reference rejects with ENOTSUP
+ * (vp8_tokens.c:357-360); SURVEY §8(f4) */
+#define VP8F_MULTI_PARTITION 2u
 int vp8f_decode_packed(ByteSpan vp8_payload, Vp8gPackedFrame* out, unsigned flags);
 /* container + key-frame header + vp8f_decode_packed; stage codes as vp8f_decode_file */
 int vp8f_decode_packed_memory(const uint8_t* data, size_t size, Vp8gPackedFrame* out, int* stage, unsigned flags);
 void vp8f_packed_free(Vp8gPackedFrame* p);
+/* RFC 6386 9.5 token partition bounds [off[p], end[p]) within the VP8 payload (off / end may be
+ * NULL to validate only).  0, or -1 + EINVAL when the size table or a partition overruns. */
+int vp8f_partition_table(ByteSpan vp8_payload, uint32_t first_partition_len, unsigned nparts, uint32_t* off,
+                         uint32_t* end);
 
 /* Host half of the device m05 (Vp8gTokFrame, include/vp8g.h): key-frame header + the first
  * partition's frame-level fields; hdr receives those fields (no arrays), tf the device job

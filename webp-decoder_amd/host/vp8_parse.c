@@ -76,7 +76,9 @@ static inline uint64_t hash_block(uint64_t h, const int16_t* blk) {
 
 typedef struct {
 	uint8_t probs[4][8][3][11]; /* token probabilities after this frame's updates */
-	Vp8Bool tok;                /* token partition */
+	Vp8Bool tok;                /* token partition (of the current MB row) */
+	Vp8Bool parts[8];           /* multi-partition streams: all token partitions */
+	unsigned nparts;
 	Vp8CoeffStats* st;
 	uint64_t hash;
 	uint64_t ovr_shift; /* shift count at which the reference-equivalent overread becomes non-zero */
@@ -176,6 +178,7 @@ typedef struct {
 	Vp8gPackedFrame* pk; /* NULL: dense */
 	int hash;            /* fold every block into the FNV-1a coefficient hash */
 	size_t cap;          /* packed: capacity of pk->values */
+	int multi;           /* accept multi-partition token streams (VP8F_MULTI_PARTITION) */
 } Sink;
 
 static int sink_values(Sink* s, uint32_t mb, uint32_t bi, const int16_t* blk, uint32_t mask) {
@@ -212,6 +215,11 @@ static int read_all_tokens(TokenCtx* t, Vp8DecodedFrame* f, const uint8_t* has_y
 	const int dense = sk->pk == NULL;
 	int16_t tmp[16], y2[16];
 	for (uint32_t r = 0; r < f->mb_rows; r++) {
+		VP8_TRACE_MARK(2, r); /* token bools of MB row r follow */
+		if (t->nparts > 1) { /* RFC 6386 9.5: MB row r reads partition r mod nparts */
+			if (r > 0) t->parts[(r - 1) % t->nparts] = t->tok;
+			t->tok = t->parts[r % t->nparts];
+		}
 		uint8_t left[9] = {0};
 		for (uint32_t c = 0; c < cols; c++) {
 			const uint32_t mb = r * cols + c;
@@ -356,6 +364,7 @@ static void parse_frame_header(ByteSpan payload, const Vp8KeyFrameHeader* kf, Vp
 	}
 
 	/* RFC 6386 9.5 token partitions */
+	VP8_TRACE_MARK(1, 0); /* the next two partition-0 bools are log2(nparts) */
 	h->nparts = 1u << vp8b_literal(hb, 2);
 
 	/* RFC 6386 9.6 quantisation */
@@ -494,17 +503,30 @@ static int decode_frame(ByteSpan payload, Vp8DecodedFrame* out, Sink* sk) {
 	st->part0_overread_bytes = vp8b_ref_overread_bytes(&hb);
 	st->part0_overread = (uint8_t)(st->part0_overread_bytes != 0);
 
-	if (nparts != 1) {
+	if (nparts != 1 && !sk->multi) { /* the reference: one token partition (vp8_tokens.c:357-360) */
 		errno = ENOTSUP;
 		goto done;
 	}
 	const size_t tok_off = 10u + kf.first_partition_len;
-	vp8b_init(&t->tok, payload.data + tok_off, payload.size - tok_off);
-	st->token_part_size_bytes = (uint32_t)(payload.size - tok_off);
 	t->st = st;
 	t->hash = 1469598103934665603ull;
-	/* overread iff (shifts >> 3) > size - min(size, 2)  (vp8b_ref_overread_bytes) */
-	t->ovr_shift = ((uint64_t)(t->tok.size - vp8b_ref_init_bytes(&t->tok)) + 1u) * 8u;
+	t->nparts = nparts;
+	if (nparts == 1) {
+		vp8b_init(&t->tok, payload.data + tok_off, payload.size - tok_off);
+		st->token_part_size_bytes = (uint32_t)(payload.size - tok_off);
+		/* overread iff (shifts >> 3) > size - min(size, 2)  (vp8b_ref_overread_bytes) */
+		t->ovr_shift = ((uint64_t)(t->tok.size - vp8b_ref_init_bytes(&t->tok)) + 1u) * 8u;
+	} else if (vp8f_partition_table(payload, kf.first_partition_len, nparts, NULL, NULL) != 0) {
+		goto done;
+	} else {
+		/* RFC 6386 9.5: 3-byte little-endian sizes of all but the last partition */
+		uint32_t off[8], end[8];
+		vp8f_partition_table(payload, kf.first_partition_len, nparts, off, end);
+		for (unsigned p = 0; p < nparts; p++) vp8b_init(&t->parts[p], payload.data + off[p], end[p] - off[p]);
+		t->tok = t->parts[0];
+		st->token_part_size_bytes = (uint32_t)(payload.size - off[0]);
+		t->ovr_shift = UINT64_MAX; /* the reference's overread diagnostics are single-partition */
+	}
 	if (read_all_tokens(t, out, has_y2, sk) != 0) goto done;
 	st->coeff_hash_fnv1a64 = sk->hash ? t->hash : 0;
 	rc = 0;
@@ -528,8 +550,29 @@ done:
 }
 
 int vp8_decode_decoded_frame(ByteSpan payload, Vp8DecodedFrame* out) {
-	Sink sk = {NULL, 1, 0};
+	Sink sk = {NULL, 1, 0, 0};
 	return decode_frame(payload, out, &sk);
+}
+
+int vp8f_partition_table(ByteSpan payload, uint32_t first_partition_len, unsigned nparts, uint32_t* off, uint32_t* end) {
+	size_t o = 10u + (size_t)first_partition_len + 3u * (nparts - 1u);
+	if (nparts < 1 || nparts > 8 || o > payload.size) {
+		errno = EINVAL;
+		return -1;
+	}
+	const uint8_t* sz = payload.data + 10u + first_partition_len;
+	for (unsigned p = 0; p < nparts; p++) {
+		const size_t len = p + 1 < nparts ? (size_t)sz[3 * p] | (size_t)sz[3 * p + 1] << 8 | (size_t)sz[3 * p + 2] << 16
+		                                  : payload.size - o;
+		if (o + len > payload.size) {
+			errno = EINVAL;
+			return -1;
+		}
+		if (off) off[p] = (uint32_t)o;
+		if (end) end[p] = (uint32_t)(o + len);
+		o += len;
+	}
+	return 0;
 }
 
 int vp8f_decode_packed(ByteSpan payload, Vp8gPackedFrame* out, unsigned flags) {
@@ -538,7 +581,7 @@ int vp8f_decode_packed(ByteSpan payload, Vp8gPackedFrame* out, unsigned flags) {
 		return -1;
 	}
 	memset(out, 0, sizeof(*out));
-	Sink sk = {out, (flags & VP8F_PACK_HASH) != 0, 0};
+	Sink sk = {out, (flags & VP8F_PACK_HASH) != 0, 0, (flags & VP8F_MULTI_PARTITION) != 0};
 	if (vp8_parse_keyframe_header(payload, &out->kf) != 0) {
 		errno = EINVAL;
 		return -1;

@@ -130,6 +130,7 @@ class Vp8gTokFrame(C.Structure):
 PK_BLOCKS = 25  # per MB: Y 0..15, U 0..3, V 0..3, Y2
 VP8G_BATCH_DEVICE_M05 = 1
 VP8F_PACK_HASH = 1
+VP8F_MULTI_PARTITION = 2
 
 ENC_FORMATS = {"rgb": 0, "ppm": 1, "png": 2}
 ENC_SPAN = 32768
@@ -299,12 +300,12 @@ def synth_frame(width: int, height: int, seed: int, profile: int = 0) -> Frame:
 class PackedFrame:
     """Owns one Vp8gPackedFrame decoded by libvp8host (vp8f_decode_packed_memory)."""
 
-    def __init__(self, data: bytes, hash_coeffs: bool = False):
+    def __init__(self, data: bytes, hash_coeffs: bool = False, multi_partition: bool = False):
         self.p = Vp8gPackedFrame()
         st = C.c_int(0)
         buf = (C.c_uint8 * len(data)).from_buffer_copy(data)
-        if host_lib().vp8f_decode_packed_memory(buf, len(data), C.byref(self.p), C.byref(st),
-                                                VP8F_PACK_HASH if hash_coeffs else 0) != 0:
+        flags = (VP8F_PACK_HASH if hash_coeffs else 0) | (VP8F_MULTI_PARTITION if multi_partition else 0)
+        if host_lib().vp8f_decode_packed_memory(buf, len(data), C.byref(self.p), C.byref(st), flags) != 0:
             raise ValueError(f"packed decode failed at stage {st.value}")
         self._alive = True
 
