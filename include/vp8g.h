@@ -226,7 +226,7 @@ typedef struct {
 /* Device m05 job of one frame: the host parses the frame header and the
  * first partition's frame-level fields (RFC 6386 9.2-9.11, 13.4); the device decodes the
  * per-macroblock modes (partition 0, from the saved bool-decoder state) and the coefficient
- * tokens (the token partition) into the batch SoA of Vp8gBatchArrays.  1216 bytes. */
+ * tokens (the token partitions) into the batch SoA of Vp8gBatchArrays.  1296 bytes. */
 typedef struct {
 	uint64_t data;       /* byte offset of the VP8 payload in the device bitstream buffer (caller) */
 	uint64_t mb_offset;  /* first MB of the frame in the batch arrays (caller) */
@@ -235,11 +235,15 @@ typedef struct {
 	uint32_t b_range;    /*   range (128..255), */
 	uint32_t b_next;     /*   payload offset of the next byte to load */
 	uint32_t p0_end;     /* payload offset one past the first partition (bytes beyond read as 0) */
-	uint32_t tok_off, tok_end; /* the token partition [tok_off, tok_end) of the payload */
+	uint32_t tok_off, tok_end; /* the (first) token partition [tok_off, tok_end) of the payload */
 	uint32_t mb_cols, mb_rows;
 	uint8_t seg_enabled, seg_map_update, use_skip, skip_prob;
 	uint8_t seg_probs[3], reserved;
 	uint8_t coeff_probs[4][8][3][12]; /* RFC 13.4 after this frame's updates; rows padded to 12 */
+	uint32_t nparts;                  /* token partitions (1, 2, 4, 8; > 1 only with VP8F_MULTI_PARTITION) */
+	uint32_t part_off[8], part_end[8]; /* partition p = [part_off[p], part_end[p]) (RFC 9.5); MB row r
+	                                      reads partition r % nparts */
+	uint32_t reserved2[3];
 } Vp8gTokFrame;
 
 /* Decode n .webp file images end to end: container/header/m05 on `threads` host threads (0 = the
@@ -256,6 +260,9 @@ int vp8g_decode_webp_batch(const ByteSpan* files, uint32_t n, int filtered, uint
  * container and the frame headers; the compressed payloads are uploaded and m05 runs on the
  * device (vp8g_m05_batch_device), one wavefront per frame.  Same outputs and errors. */
 #define VP8G_BATCH_DEVICE_M05 1u
+/* also accept multi-partition token streams (which the reference rejects, ENOTSUP), in either
+ * mode; on the device each partition gets its own wave */
+#define VP8G_BATCH_MULTI_PARTITION 2u
 int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int filtered, uint32_t threads, uint32_t flags,
                               Yuv420Image* outs, int* status);
 
@@ -329,7 +336,7 @@ int vp8g_encode_batch_device(const Vp8gEncDesc* h_descs, const Vp8gEncDesc* d_de
 const char* vp8g_last_error(void);
 
 /* ABI version of this header (bumped on any layout change). */
-#define VP8G_ABI_VERSION 4
+#define VP8G_ABI_VERSION 5
 uint32_t vp8g_abi_version(void);
 
 #ifdef __cplusplus

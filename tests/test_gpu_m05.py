@@ -113,3 +113,33 @@ def test_pipeline_device_m05_failed_frames_are_isolated(vp8g, manifest):
     assert outs[1] is None and outs[2] is None and outs[4] is None
     assert sha(outs[0]) == manifest["files"][good[0]]["yuvf_sha256"]
     assert sha(outs[3]) == manifest["files"][good[1]]["yuvf_sha256"]
+
+
+@pytest.mark.parametrize("log2k", [1, 2, 3])
+def test_m05_arrays_multi_partition(vp8g, manifest, log2k):
+    """One token wave per partition, row wavefront between them: the m05 arrays of
+    the re-partitioned frames equal the original frames' (host front end)."""
+    from multipart import repartition
+    rels = sorted(manifest["files"])[::3]
+    orig = [(FIXTURES / r).read_bytes() for r in rels]
+    got = vp8g.gpu_m05([repartition(d, log2k) for d in orig], multi_partition=True)
+    for data, g, lab in zip(orig, got, rels):
+        want = host_arrays(vp8g, data)
+        for k in NAMES:
+            assert np.array_equal(g[k], want[k]), (lab, k)
+
+
+@pytest.mark.parametrize("device_m05", [False, True])
+def test_pipeline_multi_partition(vp8g, manifest, device_m05):
+    """Multi-partition streams end to end (opt-in) reproduce the original frames' `-yuvf` output;
+    without the flag they fail like the reference (ENOTSUP) and the rest of the batch decodes."""
+    from multipart import repartition
+    rels = sorted(manifest["files"])[::4] + ["big/uhd_a_normal_seg4.webp", "big/uhd_d_normal_q90.webp"]
+    files = [repartition((FIXTURES / r).read_bytes(), 1 + i % 3) for i, r in enumerate(rels)]
+    outs, st = vp8g.gpu_decode_webp_batch(files, True, 8, device_m05=device_m05, multi_partition=True)
+    assert st == [0] * len(rels)
+    bad = [r for r, o in zip(rels, outs) if sha(o) != manifest["files"][r]["yuvf_sha256"]]
+    assert not bad, bad[:8]
+    outs, st = vp8g.gpu_decode_webp_batch(files[:3] + [(FIXTURES / rels[0]).read_bytes()], True, 4,
+                                          device_m05=device_m05)
+    assert all(s != 0 for s in st[:3]) and st[3] == 0

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol(vp8g):
     lib = vp8g.gpu_lib()
     missing = [f for f in header_functions() if not hasattr(lib, f)]
     assert not missing, missing
-    assert lib.vp8g_abi_version() == 4
+    assert lib.vp8g_abi_version() == 5
 
 
 def test_struct_layouts(vp8g):

@@ -57,3 +57,18 @@ def test_partition_table_rejects_overruns(vp8g, manifest):
     m[20 + 10 + fpl:20 + 10 + fpl + 3] = b"\xff\xff\xff"  # first partition size past the end
     with pytest.raises(ValueError):
         vp8g.PackedFrame(bytes(m), multi_partition=True)
+
+
+def test_token_header_partition_table(vp8g, manifest):
+    """The device job of a multi-partition frame lists the partitions (opt-in), contiguous after
+    the size table, the last one ending at the payload's end."""
+    data = (FIXTURES / sorted(manifest["files"])[7]).read_bytes()
+    for log2k in (1, 2, 3):
+        m = repartition(data, log2k)
+        with pytest.raises(ValueError):
+            vp8g.token_header(m)
+        kf, hdr, tf, off, size = vp8g.token_header(m, multi_partition=True)
+        k = 1 << log2k
+        assert tf.nparts == k
+        assert tf.part_off[0] == 10 + kf.first_partition_len + 3 * (k - 1) == tf.tok_off
+        assert all(tf.part_off[p + 1] == tf.part_end[p] for p in range(k - 1)) and tf.part_end[k - 1] == size

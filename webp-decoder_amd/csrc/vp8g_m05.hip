@@ -245,23 +245,35 @@ DEV bool read_block(DBool& b, const uint8_t* pl, const TypeTab& t, uint32_t firs
 	return nz;
 }
 
-// Per-frame workgroup of two waves, one per partition (their chains are independent):
+// Per-frame workgroup: one wave per arithmetic-coded chain (the chains are independent).
 //   wave 0 ("modes") decodes partition 0 -- segment, skip flag, luma / chroma / sub-block modes --
-//          writes the mode arrays and, per MB, a flag byte (skip, has Y2) into an LDS ring;
-//   wave 1 ("tokens") decodes the token partition MB by MB as the ring fills.
-// The token chain is the long one; taking the modes off it shortens the frame's critical path.
-// Ring protocol (LDS only, one writer per word): the modes wave writes ring[m] and then
-// prod = m + 1; the tokens wave reads prod, then ring[m]; it publishes cons every 64 MBs and the
-// modes wave stays less than kRing MBs ahead of it.  LDS operations of a wave complete in order,
-// so volatile accesses (no compiler reordering) are enough; s_sleep while waiting.
-constexpr uint32_t kRing = 1024;
+//          and writes the mode arrays and, per MB, a flag byte (skip, has Y2) into an LDS ring;
+//   waves 1..n ("tokens", one per token partition, RFC 6386 9.5) decode MB rows r = w, w + n, ...
+//          from partition w as the ring fills.  With n > 1 the token waves form a row wavefront:
+//          MB (r, c) needs the above contexts row r - 1 leaves at column c.
+// Taking the modes off the token chain and splitting the tokens by rows shortens the frame's
+// critical path; a single-partition frame has one token wave.
+// Protocol (LDS only, one writer per word): the modes wave writes ring[m] and then prod = m + 1;
+// token wave w publishes done[w] = index + 1 of the last MB it finished (all MBs once it runs
+// out of rows).  A token wave waits for prod > m and for done[wave of row r - 1] past column c;
+// the modes wave stays less than kRing MBs ahead of min(done).  LDS operations of a wave complete
+// in order, so volatile accesses (no compiler reordering) suffice; s_sleep while waiting; waits
+// are bounded (VP8G_ERR_TIMEOUT) so a broken stream cannot keep the grid alive.
+constexpr uint32_t kRing = 8192;          // >= 8 MB rows of a 1024-MB-wide frame in flight
+constexpr uint32_t kMaxParts = 8;
 constexpr uint32_t kMaxPolls = 1u << 24;  // a few seconds of s_sleep
+constexpr uint32_t kCtlWords = 1u + kMaxParts;
 // LDS pointers typed as such: a volatile generic pointer would become flat accesses, whose
 // completion the compiler tracks with vmcnt (so every poll would also wait for the wave's stores)
 typedef __attribute__((address_space(3))) volatile uint32_t lds_u32;
 typedef __attribute__((address_space(3))) volatile uint8_t lds_u8;
 
-DEV void modes_wave(const Vp8gTokFrame& J, const uint8_t* pl, Out o, lds_u32* ctl, lds_u8* ring, lds_u32* above_b) {
+DEV void timeout(const Out& o) {
+	if (lane() == 0) atomicOr(o.status, VP8G_ERR_TIMEOUT);
+}
+
+DEV void modes_wave(const Vp8gTokFrame& J, const uint8_t* pl, Out o, lds_u32* ctl, lds_u8* ring, lds_u32* above_b,
+                    uint32_t nparts) {
 	const uint32_t L = lane(), cols = J.mb_cols, rows = J.mb_rows;
 	uint32_t bl[3], bh[3];  // sub-block mode rows 0..63 / 64..99 in lanes
 #pragma unroll
@@ -282,11 +294,13 @@ DEV void modes_wave(const Vp8gTokFrame& J, const uint8_t* pl, Out o, lds_u32* ct
 		for (uint32_t c = 0; c < cols; c++, m++) {
 			for (uint32_t polls = 0; m - cons >= kRing; polls++) {
 				if (polls == kMaxPolls) {
-					if (L == 0) atomicOr(o.status, VP8G_ERR_TIMEOUT);
+					timeout(o);
 					break;
 				}
 				__builtin_amdgcn_s_sleep(2);
-				cons = __builtin_amdgcn_readfirstlane(ctl[1]);
+				uint32_t lo = 0xFFFFFFFFu;
+				for (uint32_t w = 0; w < nparts; w++) lo = min(lo, (uint32_t)__builtin_amdgcn_readfirstlane(ctl[1 + w]));
+				cons = lo;
 			}
 			const uint64_t mb = J.mb_offset + m;
 			const uint32_t ab = __builtin_amdgcn_readfirstlane(above_b[c]);
@@ -331,7 +345,8 @@ DEV void modes_wave(const Vp8gTokFrame& J, const uint8_t* pl, Out o, lds_u32* ct
 	}
 }
 
-DEV void tokens_wave(const Vp8gTokFrame& J, const uint8_t* pl, Out o, lds_u32* ctl, lds_u8* ring, lds_u32* above) {
+DEV void tokens_wave(const Vp8gTokFrame& J, const uint8_t* pl, Out o, lds_u32* ctl, lds_u8* ring, lds_u32* above,
+                     uint32_t w, uint32_t nparts) {
 	const uint32_t L = lane(), cols = J.mb_cols, rows = J.mb_rows;
 	// coefficient rows of the 4 block types in lanes (TypeTab)
 	const uint32_t* const cp = (const uint32_t*)J.coeff_probs;  // [4][24] rows of 3 dwords
@@ -342,20 +357,33 @@ DEV void tokens_wave(const Vp8gTokFrame& J, const uint8_t* pl, Out o, lds_u32* c
 #pragma unroll
 	for (int k = 0; k < 2; k++) vb[k] = (L & 31u) < 24u ? cp[(2 * k + (L >> 5)) * 72 + (L & 31u) * 3 + 2] : 0u;
 	DBool tb;
-	dinit(tb, pl, 0, -8, 255u, J.tok_off, J.tok_end);
+	dinit(tb, pl, 0, -8, 255u, J.part_off[w], J.part_end[w]);
 	dfill(tb, pl);
-	uint32_t m = 0, prod = 0;
-	for (uint32_t r = 0; r < rows; r++) {
+	const uint32_t prev = (w + nparts - 1u) % nparts;  // the wave of row r - 1
+	uint32_t prod = 0, up = 0;
+	for (uint32_t r = w; r < rows; r += nparts) {
 		uint32_t left = 0;  // token contexts, bits as in above[]
-		for (uint32_t c = 0; c < cols; c++, m++) {
+		for (uint32_t c = 0; c < cols; c++) {
+			const uint32_t m = r * cols + c;
 			for (uint32_t polls = 0; m >= prod; polls++) {
 				if (polls == kMaxPolls) {
-					if (L == 0) atomicOr(o.status, VP8G_ERR_TIMEOUT);
+					timeout(o);
 					prod = m + 1u;
 					break;
 				}
 				prod = __builtin_amdgcn_readfirstlane(ctl[0]);
 				if (m >= prod) __builtin_amdgcn_s_sleep(1);
+			}
+			if (nparts > 1 && r > 0) {  // row wavefront: MB (r - 1, c) done
+				for (uint32_t polls = 0; up < m - cols + 1u; polls++) {
+					if (polls == kMaxPolls) {
+						timeout(o);
+						up = m;
+						break;
+					}
+					up = __builtin_amdgcn_readfirstlane(ctl[1 + prev]);
+					if (up < m - cols + 1u) __builtin_amdgcn_s_sleep(1);
+				}
 			}
 			const uint32_t fl = __builtin_amdgcn_readfirstlane(ring[m & (kRing - 1u)]);
 			const uint64_t mb = J.mb_offset + m;
@@ -395,30 +423,32 @@ DEV void tokens_wave(const Vp8gTokFrame& J, const uint8_t* pl, Out o, lds_u32* c
 			}
 			if (L == 0) {
 				above[c] = ab;
-				if ((m & 63u) == 63u) ctl[1] = m + 1u;
+				if (nparts > 1 || (m & 63u) == 63u) ctl[1 + w] = m + 1u;
 			}
 			o.hasc[mb] = (uint8_t)any;
 		}
 	}
+	if (L == 0) ctl[1 + w] = 0xFFFFFFFFu;  // out of rows: never the one anybody waits for
 }
 
-// LDS: ctl[2] (prod, cons), ring[kRing] flag bytes, then per MB column the token contexts
-// (bits 0..8: Y 0..3, U 4..5, V 6..7, Y2 8) and the bottom row's sub-block modes (4 nibbles;
-// B_DC = 0 above the frame).
-__global__ __launch_bounds__(128) void m05_kernel(const Vp8gTokFrame* __restrict__ jobs, const uint8_t* __restrict__ bits,
-                                                  Out o) {
+// LDS: ctl[kCtlWords] (prod, done[8]), ring[kRing] flag bytes, then per MB column the token
+// contexts (bits 0..8: Y 0..3, U 4..5, V 6..7, Y2 8) and the bottom row's sub-block modes
+// (4 nibbles; B_DC = 0 above the frame).
+__global__ __launch_bounds__(64 * (1 + kMaxParts)) void m05_kernel(const Vp8gTokFrame* __restrict__ jobs,
+                                                                   const uint8_t* __restrict__ bits, Out o) {
 	extern __shared__ uint32_t sm[];
 	const Vp8gTokFrame& J = jobs[blockIdx.x];
-	const uint32_t cols = J.mb_cols;
-	const uint32_t words = 2u + kRing / 4u + 2u * cols;
-	for (uint32_t i = threadIdx.x; i < words; i += 128u) sm[i] = 0;
+	const uint32_t cols = J.mb_cols, nparts = J.nparts;
+	const uint32_t words = kCtlWords + kRing / 4u + 2u * cols;
+	for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) sm[i] = 0;
 	__syncthreads();
 	lds_u32* const ctl = (lds_u32*)sm;
-	lds_u8* const ring = (lds_u8*)(sm + 2);
-	lds_u32* const above = (lds_u32*)(sm + 2 + kRing / 4u);
+	lds_u8* const ring = (lds_u8*)(sm + kCtlWords);
+	lds_u32* const above = (lds_u32*)(sm + kCtlWords + kRing / 4u);
 	const uint8_t* pl = bits + J.data;
-	if ((__builtin_amdgcn_readfirstlane(threadIdx.x) >> 6) == 0) modes_wave(J, pl, o, ctl, ring, above + cols);
-	else tokens_wave(J, pl, o, ctl, ring, above);
+	const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
+	if (wave == 0) modes_wave(J, pl, o, ctl, ring, above + cols, nparts);
+	else if (wave <= nparts) tokens_wave(J, pl, o, ctl, ring, above, wave - 1u, nparts);
 }
 
 }  // namespace
@@ -429,16 +459,20 @@ VP8G_API int vp8g_m05_batch_device(const Vp8gTokFrame* h_jobs, const Vp8gTokFram
 		errno = EINVAL;
 		return -1;
 	}
-	uint32_t max_cols = 0;
+	uint32_t max_cols = 0, max_parts = 1;
 	for (uint32_t i = 0; i < n; i++) {
 		const Vp8gTokFrame& j = h_jobs[i];
-		if (j.mb_cols == 0 || j.mb_cols > 1024u || j.mb_rows == 0 || j.mb_rows > 1024u || (j.data & 3u) ||
-		    j.tok_end < j.tok_off || j.p0_end > j.tok_end || j.b_next > j.p0_end || j.b_bits < 0 || j.b_bits > 56 ||
-		    j.b_range < 128u || j.b_range > 255u) {
+		bool ok = j.mb_cols > 0 && j.mb_cols <= 1024u && j.mb_rows > 0 && j.mb_rows <= 1024u && !(j.data & 3u) &&
+		          j.b_next <= j.p0_end && j.b_bits >= 0 && j.b_bits <= 56 && j.b_range >= 128u && j.b_range <= 255u &&
+		          (j.nparts == 1 || j.nparts == 2 || j.nparts == 4 || j.nparts == 8);
+		for (uint32_t p = 0; ok && p < j.nparts; p++)
+			ok = j.part_off[p] >= j.p0_end && j.part_end[p] >= j.part_off[p] && (p == 0 || j.part_off[p] >= j.part_end[p - 1]);
+		if (!ok) {
 			errno = EINVAL;
 			return -1;
 		}
 		if (j.mb_cols > max_cols) max_cols = j.mb_cols;
+		if (j.nparts > max_parts) max_parts = j.nparts;
 	}
 	Out o;
 	o.cy = const_cast<int16_t*>(arrays->coeff_y);
@@ -451,8 +485,8 @@ VP8G_API int vp8g_m05_batch_device(const Vp8gTokFrame* h_jobs, const Vp8gTokFram
 	o.hasc = const_cast<uint8_t*>(arrays->has_coeff);
 	o.bmode = const_cast<uint8_t*>(arrays->bmode);
 	o.status = arrays->status;
-	hipLaunchKernelGGL(m05_kernel, dim3(n), dim3(128), (2u + kRing / 4u + 2u * max_cols) * 4u, (hipStream_t)hip_stream,
-	                   d_jobs, d_bits, o);
+	hipLaunchKernelGGL(m05_kernel, dim3(n), dim3(64u * (1u + max_parts)), (kCtlWords + kRing / 4u + 2u * max_cols) * 4u,
+	                   (hipStream_t)hip_stream, d_jobs, d_bits, o);
 	const hipError_t e = hipGetLastError();
 	if (e != hipSuccess) {
 		vp8g::set_error_text("m05 launch", e);

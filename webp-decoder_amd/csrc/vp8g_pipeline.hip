@@ -112,6 +112,7 @@ struct Feed {
 	const ByteSpan* files = nullptr;
 	uint32_t n = 0;
 	bool tok = false;  // device m05: workers fill tj instead of pk
+	unsigned fflags = 0;  // front-end flags (VP8F_MULTI_PARTITION)
 	std::vector<Vp8gPackedFrame> pk;
 	std::vector<TokJob> tj;
 	std::vector<int> err;
@@ -135,9 +136,10 @@ struct Feed {
 			if (!files[i].data) e = EINVAL;
 			else if (tok) {
 				TokJob& j = tj[i];
-				if (vp8f_token_header_memory(files[i].data, files[i].size, &j.kf, &j.hdr, &j.tf, &j.poff, &j.psize, &stage) != 0)
+				if (vp8f_token_header_memory(files[i].data, files[i].size, &j.kf, &j.hdr, &j.tf, &j.poff, &j.psize, &stage,
+				                             fflags) != 0)
 					e = errno ? errno : EINVAL;
-			} else if (vp8f_decode_packed_memory(files[i].data, files[i].size, &pk[i], &stage, 0) != 0)
+			} else if (vp8f_decode_packed_memory(files[i].data, files[i].size, &pk[i], &stage, fflags) != 0)
 				e = errno ? errno : EINVAL;
 			{
 				std::lock_guard<std::mutex> lk(mu);
@@ -200,7 +202,7 @@ hipError_t grow(Slot& s, size_t need) {
 
 VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int filtered, uint32_t threads, uint32_t flags,
                                        Yuv420Image* outs, int* status) {
-	if (!files || !outs || n == 0 || (flags & ~VP8G_BATCH_DEVICE_M05)) {
+	if (!files || !outs || n == 0 || (flags & ~(VP8G_BATCH_DEVICE_M05 | VP8G_BATCH_MULTI_PARTITION))) {
 		errno = EINVAL;
 		return -1;
 	}
@@ -219,6 +221,7 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 	feed.files = files;
 	feed.n = n;
 	feed.tok = tok;
+	feed.fflags = (flags & VP8G_BATCH_MULTI_PARTITION) ? VP8F_MULTI_PARTITION : 0u;
 	if (tok) feed.tj.assign(n, TokJob{});
 	else feed.pk.assign(n, Vp8gPackedFrame{});
 	feed.err.assign(n, 0);

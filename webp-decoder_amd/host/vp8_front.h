@@ -61,13 +61,16 @@ int vp8f_partition_table(ByteSpan vp8_payload, uint32_t first_partition_len, uns
 
 /* Host half of the device m05 (Vp8gTokFrame, include/vp8g.h): key-frame header + the first
  * partition's frame-level fields; hdr receives those fields (no arrays), tf the device job
- * (data / mb_offset left 0 for the caller).  0, or -1 + errno (EINVAL, ENOTSUP). */
-int vp8f_token_header(ByteSpan vp8_payload, Vp8KeyFrameHeader* kf, Vp8DecodedFrame* hdr, Vp8gTokFrame* tf);
+ * (data / mb_offset left 0 for the caller).  flags: VP8F_MULTI_PARTITION accepts 2/4/8 token
+ * partitions.  0, or -1 + errno (EINVAL, ENOTSUP). */
+int vp8f_token_header(ByteSpan vp8_payload, Vp8KeyFrameHeader* kf, Vp8DecodedFrame* hdr, Vp8gTokFrame* tf,
+                      unsigned flags);
 /* container + vp8f_token_header; *payload_off / *payload_size locate the VP8 payload in data.
  * Stage codes as vp8f_decode_file (2 container, 3 not a key frame / bad frame header, 4 first
  * partition or unsupported partitioning). */
 int vp8f_token_header_memory(const uint8_t* data, size_t size, Vp8KeyFrameHeader* kf, Vp8DecodedFrame* hdr,
-                             Vp8gTokFrame* tf, uint64_t* payload_off, uint32_t* payload_size, int* stage);
+                             Vp8gTokFrame* tf, uint64_t* payload_off, uint32_t* payload_size, int* stage,
+                             unsigned flags);
 
 /* Seeded synthetic Vp8DecodedFrame (build-defined generator, see vp8_synth.c header for the
  * exact distribution).  profile 0 = "measured-like" statistics, 1 = stress (full-range coeffs,

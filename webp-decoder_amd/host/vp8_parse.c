@@ -589,7 +589,7 @@ int vp8f_decode_packed(ByteSpan payload, Vp8gPackedFrame* out, unsigned flags) {
 	return decode_frame(payload, &out->f, &sk);
 }
 
-int vp8f_token_header(ByteSpan payload, Vp8KeyFrameHeader* kf, Vp8DecodedFrame* hdr, Vp8gTokFrame* tf) {
+int vp8f_token_header(ByteSpan payload, Vp8KeyFrameHeader* kf, Vp8DecodedFrame* hdr, Vp8gTokFrame* tf, unsigned flags) {
 	if (!kf || !hdr || !tf) {
 		errno = EINVAL;
 		return -1;
@@ -610,15 +610,18 @@ int vp8f_token_header(ByteSpan payload, Vp8KeyFrameHeader* kf, Vp8DecodedFrame* 
 	hdr->mb_total = hdr->stats.mb_total = cols * rows;
 	FrameHdr fh;
 	parse_frame_header(payload, kf, hdr, &fh);
-	if (fh.nparts != 1) { /* the reference's m05 supports one token partition (vp8_tokens.c:357-360) */
+	if (fh.nparts != 1 && !(flags & VP8F_MULTI_PARTITION)) { /* the reference: one token partition
+	                                                            (vp8_tokens.c:357-360) */
 		errno = ENOTSUP;
 		return -1;
 	}
+	if (vp8f_partition_table(payload, kf->first_partition_len, fh.nparts, tf->part_off, tf->part_end) != 0) return -1;
+	tf->nparts = fh.nparts;
 	tf->mb_cols = cols;
 	tf->mb_rows = rows;
 	tf->p0_end = 10u + kf->first_partition_len;
-	tf->tok_off = tf->p0_end;
-	tf->tok_end = (uint32_t)payload.size;
+	tf->tok_off = tf->part_off[0];
+	tf->tok_end = tf->part_end[0];
 	tf->b_next = (uint32_t)(fh.hb.next - payload.data);
 	tf->b_value = fh.hb.value;
 	tf->b_bits = fh.hb.bits;

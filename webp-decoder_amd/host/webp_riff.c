@@ -126,7 +126,8 @@ int vp8f_decode_packed_memory(const uint8_t* data, size_t size, Vp8gPackedFrame*
 }
 
 int vp8f_token_header_memory(const uint8_t* data, size_t size, Vp8KeyFrameHeader* kf, Vp8DecodedFrame* hdr,
-                             Vp8gTokFrame* tf, uint64_t* payload_off, uint32_t* payload_size, int* stage) {
+                             Vp8gTokFrame* tf, uint64_t* payload_off, uint32_t* payload_size, int* stage,
+                             unsigned flags) {
 	int st = 0, rc = -1;
 	WebPContainer c;
 	ByteSpan file = {data, size};
@@ -143,7 +144,7 @@ int vp8f_token_header_memory(const uint8_t* data, size_t size, Vp8KeyFrameHeader
 		if (vp8_parse_keyframe_header(payload, kf) != 0 || !kf->is_key_frame) {
 			errno = EINVAL;
 			st = 3;
-		} else if (vp8f_token_header(payload, kf, hdr, tf) != 0) {
+		} else if (vp8f_token_header(payload, kf, hdr, tf, flags) != 0) {
 			st = 4;
 		} else {
 			*payload_off = c.vp8_chunk_offset;

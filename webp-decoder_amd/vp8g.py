@@ -124,11 +124,13 @@ class Vp8gTokFrame(C.Structure):
                 ("tok_end", C.c_uint32), ("mb_cols", C.c_uint32), ("mb_rows", C.c_uint32),
                 ("seg_enabled", C.c_uint8), ("seg_map_update", C.c_uint8), ("use_skip", C.c_uint8),
                 ("skip_prob", C.c_uint8), ("seg_probs", C.c_uint8 * 3), ("reserved", C.c_uint8),
-                ("coeff_probs", C.c_uint8 * (4 * 8 * 3 * 12))]
+                ("coeff_probs", C.c_uint8 * (4 * 8 * 3 * 12)), ("nparts", C.c_uint32),
+                ("part_off", C.c_uint32 * 8), ("part_end", C.c_uint32 * 8), ("reserved2", C.c_uint32 * 3)]
 
 
 PK_BLOCKS = 25  # per MB: Y 0..15, U 0..3, V 0..3, Y2
 VP8G_BATCH_DEVICE_M05 = 1
+VP8G_BATCH_MULTI_PARTITION = 2
 VP8F_PACK_HASH = 1
 VP8F_MULTI_PARTITION = 2
 
@@ -141,7 +143,7 @@ assert C.sizeof(Vp8CoeffStats) == 200
 assert C.sizeof(Vp8DecodedFrame) == 320
 assert C.sizeof(Yuv420Image) == 40
 assert C.sizeof(Vp8gFrameDesc) == 176
-assert C.sizeof(Vp8gTokFrame) == 1216
+assert C.sizeof(Vp8gTokFrame) == 1296
 
 VP8G_F_LOOPFILTER = 1
 VP8G_F_SIMPLE = 2
@@ -192,7 +194,8 @@ def host_lib():
         lib.vp8f_packed_free.argtypes = [C.POINTER(Vp8gPackedFrame)]
         lib.vp8f_token_header_memory.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(Vp8KeyFrameHeader),
                                                  C.POINTER(Vp8DecodedFrame), C.POINTER(Vp8gTokFrame),
-                                                 C.POINTER(C.c_uint64), C.POINTER(C.c_uint32), C.POINTER(C.c_int)]
+                                                 C.POINTER(C.c_uint64), C.POINTER(C.c_uint32), C.POINTER(C.c_int),
+                                                 C.c_uint]
         lib.vp8f_packed_free.restype = None
         lib._typed = True
     return lib
@@ -350,24 +353,24 @@ def unpack_coeffs(pf: PackedFrame) -> dict:
             "coeff_v": dense[:, 20:24].reshape(-1), "coeff_y2": dense[:, 24].reshape(-1)}
 
 
-def token_header(data: bytes):
+def token_header(data: bytes, multi_partition: bool = False):
     """vp8f_token_header_memory: (kf, hdr, Vp8gTokFrame, payload offset, payload size) or raises."""
     lib = host_lib()
     kf, hdr, tf = Vp8KeyFrameHeader(), Vp8DecodedFrame(), Vp8gTokFrame()
     off, size, st = C.c_uint64(0), C.c_uint32(0), C.c_int(0)
     buf = (C.c_uint8 * max(1, len(data))).from_buffer_copy(data or b"\0")
     if lib.vp8f_token_header_memory(buf, len(data), C.byref(kf), C.byref(hdr), C.byref(tf), C.byref(off),
-                                    C.byref(size), C.byref(st)) != 0:
+                                    C.byref(size), C.byref(st), VP8F_MULTI_PARTITION if multi_partition else 0) != 0:
         raise ValueError(f"vp8f_token_header_memory: stage {st.value}")
     return kf, hdr, tf, off.value, size.value
 
 
-def gpu_m05(files: list[bytes]) -> list[dict]:
+def gpu_m05(files: list[bytes], multi_partition: bool = False) -> list[dict]:
     """vp8g_m05_batch_device over .webp images (one launch): per frame the m05 arrays as numpy,
     named as FRAME_ARRAYS (skip_coeff excepted: the device does not keep it)."""
     import torch
     lib = gpu_lib()
-    hdrs = [token_header(b) for b in files]
+    hdrs = [token_header(b, multi_partition) for b in files]
     n = len(files)
     jobs = (Vp8gTokFrame * n)()
     slots, mbs = [], []
@@ -405,7 +408,8 @@ def gpu_m05(files: list[bytes]) -> list[dict]:
     return out
 
 
-def gpu_decode_webp_batch(files: list[bytes], filtered: bool = True, threads: int = 0, device_m05: bool = False):
+def gpu_decode_webp_batch(files: list[bytes], filtered: bool = True, threads: int = 0, device_m05: bool = False,
+                          multi_partition: bool = False):
     """vp8g_decode_webp_batch(_ex): .webp images -> (list of I420 bytes or None, list of errno).
     device_m05: m05 on the device (VP8G_BATCH_DEVICE_M05) instead of the host threads."""
     lib = gpu_lib()
@@ -417,7 +421,8 @@ def gpu_decode_webp_batch(files: list[bytes], filtered: bool = True, threads: in
     import time
     t0 = time.perf_counter()
     rc = lib.vp8g_decode_webp_batch_ex(spans, n, int(filtered), threads,
-                                       VP8G_BATCH_DEVICE_M05 if device_m05 else 0, imgs, st)
+                                       (VP8G_BATCH_DEVICE_M05 if device_m05 else 0)
+                                       | (VP8G_BATCH_MULTI_PARTITION if multi_partition else 0), imgs, st)
     gpu_decode_webp_batch.seconds = time.perf_counter() - t0  # the C call alone (no Python copies)
     if rc != 0 and all(s == 5 for s in st):  # EIO: device failure, nothing returned
         raise RuntimeError(f"vp8g_decode_webp_batch failed: {lib.vp8g_last_error()!r}")
