@@ -2,6 +2,7 @@
 launch.  Usage: python tools/m05_kernel_probe.py [fixture-index 0..3] [N ...]"""
 import ctypes as C
 import json
+import os
 import pathlib
 import sys
 
@@ -17,7 +18,12 @@ from bench import FIXTURES  # noqa: E402
 fi = int(sys.argv[1]) if len(sys.argv) > 1 else 0
 ns = [int(a) for a in sys.argv[2:]] or [1, 64, 256, 1024]
 data = (ROOT / "tests" / "fixtures" / FIXTURES[fi]).read_bytes()
-kf, hdr, tf, off, size = vp8g.token_header(data)
+log2k = int(os.environ.get("M05_LOG2K", "0"))  # re-encode over 2^k token partitions (test generator)
+if log2k:
+    sys.path.insert(0, str(ROOT / "tests"))
+    from multipart import repartition  # noqa: E402
+    data = repartition(data, log2k)
+kf, hdr, tf, off, size = vp8g.token_header(data, multi_partition=log2k > 0)
 lib = vp8g.gpu_lib()
 dev = torch.device("cuda:0")
 slot = (size + 512 + 15) & ~15
@@ -45,7 +51,7 @@ for n in ns:
         torch.cuda.synchronize()
         times.append(e0.elapsed_time(e1))
     ms = min(times)
-    print(json.dumps({"fixture": FIXTURES[fi], "payload_bytes": size, "frames": n, "ms": round(ms, 2),
+    print(json.dumps({"fixture": FIXTURES[fi], "partitions": 1 << log2k, "payload_bytes": size, "frames": n, "ms": round(ms, 2),
                       "frames_per_s": round(n / ms * 1e3, 1), "MB_per_s_compressed": round(n * size / ms / 1e3, 1),
                       "MP_per_s": round(n * 3840 * 2160 / ms / 1e3, 1)}), flush=True)
     del d_bits, d_jobs, arr_t
