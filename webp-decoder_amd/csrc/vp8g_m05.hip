@@ -85,7 +85,7 @@ DEV uint32_t rl(uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_read
 struct DBool {
 	uint64_t value;
 	int bits;
-	uint32_t range;
+	uint32_t range;  // range - 1 (saves the two +-1 of the split on the chain)
 	uint32_t next, end;
 	uint32_t base;       // window start (4-aligned)
 	uint32_t cur, nxt;   // per lane: dword base/4 + lane, big-endian (cur); + 64, as loaded (nxt)
@@ -97,7 +97,7 @@ struct DBool {
 DEV uint32_t win_load(const uint8_t* pl, uint32_t at) { return *(const uint32_t*)(pl + at + 4u * lane()); }
 
 DEV void dinit(DBool& b, const uint8_t* pl, uint64_t value, int bits, uint32_t range, uint32_t next, uint32_t end) {
-	b.value = value, b.bits = bits, b.range = range, b.next = next, b.end = end;
+	b.value = value, b.bits = bits, b.range = range - 1u, b.next = next, b.end = end;
 	b.base = next & ~3u;
 	b.cur = __builtin_bswap32(win_load(pl, b.base));
 	b.nxt = win_load(pl, b.base + 256u);
@@ -125,18 +125,18 @@ DEV void dfill(DBool& b, const uint8_t* pl) {
 }
 
 DEV uint32_t dread(DBool& b, const uint8_t* pl, uint32_t prob) {
-	const uint32_t split = 1u + (((b.range - 1u) * prob) >> 8);
-	uint32_t bit;
-	if ((uint32_t)(b.value >> b.bits) >= split) {  // 64-bit shift + 32-bit compare: both scalar
-		b.value -= (uint64_t)split << b.bits;
-		b.range -= split;
+	const uint32_t split = (b.range * prob) >> 8;  // RFC 6386 7.3 split - 1
+	uint32_t bit, r;
+	if ((uint32_t)(b.value >> b.bits) > split) {  // 64-bit shift + 32-bit compare: both scalar
+		b.value -= (uint64_t)(split + 1u) << b.bits;
+		r = b.range - split;  // new range (not minus 1)
 		bit = 1u;
 	} else {
-		b.range = split;
+		r = split + 1u;
 		bit = 0u;
 	}
-	const int sh = __builtin_clz(b.range) - 24;
-	b.range <<= sh;
+	const int sh = __builtin_clz(r) - 24;
+	b.range = (r << sh) - 1u;
 	b.bits -= sh;
 	if (b.bits < 0) dfill(b, pl);
 	return bit;
