@@ -72,3 +72,39 @@ def test_token_header_partition_table(vp8g, manifest):
         assert tf.nparts == k
         assert tf.part_off[0] == 10 + kf.first_partition_len + 3 * (k - 1) == tf.tok_off
         assert all(tf.part_off[p + 1] == tf.part_end[p] for p in range(k - 1)) and tf.part_end[k - 1] == size
+
+
+def test_m05_launcher_validates_jobs(vp8g, manifest):
+    """vp8g_m05_batch_device checks every job on the host before anything reaches the device
+    (inconsistent jobs -> EINVAL, no launch): partition counts, partition order, bool state,
+    dimensions, alignment, and the required status word.  Runs without a GPU."""
+    import ctypes as C
+    lib = vp8g.gpu_lib()
+    data = repartition((FIXTURES / sorted(manifest["files"])[5]).read_bytes(), 2)
+    _, _, tf, _, _ = vp8g.token_header(data, multi_partition=True)
+    status = C.c_uint32(0)
+    arr = vp8g.Vp8gBatchArrays(**{k: 16 for k in ("coeff_y", "coeff_u", "coeff_v", "coeff_y2", "ymode", "uv_mode",
+                                                  "segment_id", "has_coeff", "bmode")},
+                               src=None, status=C.addressof(status))
+
+    def call(job, arrays=arr):
+        jobs = (vp8g.Vp8gTokFrame * 1)(job)
+        C.set_errno(0)
+        return lib.vp8g_m05_batch_device(jobs, 16, 1, 16, C.byref(arrays), None)
+
+    def bad(**fields):
+        j = vp8g.Vp8gTokFrame.from_buffer_copy(bytes(tf))
+        for k, v in fields.items():
+            if isinstance(v, tuple):
+                getattr(j, k)[v[0]] = v[1]
+            else:
+                setattr(j, k, v)
+        return j
+
+    for job in (bad(nparts=3), bad(nparts=16), bad(mb_cols=0), bad(mb_rows=2000), bad(data=2), bad(b_range=300),
+                bad(b_bits=-1), bad(b_next=tf.p0_end + 1), bad(part_off=(1, tf.part_end[0] - 1)),
+                bad(part_off=(0, tf.p0_end - 1))):
+        assert call(job) == -1 and C.get_errno() == 22
+    no_status = vp8g.Vp8gBatchArrays.from_buffer_copy(bytes(arr))
+    no_status.status = None
+    assert call(tf, no_status) == -1 and C.get_errno() == 22

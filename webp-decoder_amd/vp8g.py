@@ -172,7 +172,7 @@ def _load(name: str, path: pathlib.Path):
     if name not in _libs:
         if not path.exists():
             raise OSError(f"{path} not built (run `make` at the repo root)")
-        _libs[name] = C.CDLL(str(path))
+        _libs[name] = C.CDLL(str(path), use_errno=True)
     return _libs[name]
 
 
