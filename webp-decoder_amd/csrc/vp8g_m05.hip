@@ -1,16 +1,15 @@
 // vp8g_m05.hip -- m05 on the device: per-macroblock modes and coefficient
-// tokens of a batch of key frames, one wavefront per frame.
+// tokens of a batch of key frames, one workgroup per frame.
 //
 // VP8's arithmetic-coded partitions are serial chains (each bool's range depends on the previous
-// one), and a key frame with one token partition has exactly two of them: partition 0 (modes) and
-// the token partition.  There is no parallelism inside a frame, so the unit of parallelism is the
-// frame: one 64-thread workgroup decodes one frame with wave-uniform code.  Every value on the
-// decode chain is the same in all lanes, so the decoder state lives in scalar registers and the
-// bool decoder runs on the scalar ALU.  The chain is latency-bound, so nothing on it waits for
-// memory: the probability tables and a window of each partition sit in VGPR lanes and are read
-// with v_readlane (see "register tables" below).  A batch of a few hundred frames gives every CU
-// one or more frames.  The two chains are interleaved MB by MB (modes of MB m, then its tokens):
-// they are independent streams read in the same raster order.
+// one): partition 0 (modes) and one token partition per 1, 2, 4 or 8 (RFC 6386 9.5; the
+// reference supports one).  Inside a chain there is no parallelism, so a frame gets one wave per
+// chain -- a modes wave and a token wave per partition, coupled through LDS (see "Per-frame
+// workgroup" below) -- and the chip is filled with frames.  Every value on a chain is the same in
+// all lanes, so the decoder state lives in scalar registers and the bool decoder runs on the
+// scalar ALU.  The chains are latency-bound, so nothing on them waits for memory: the probability
+// tables and a window of each partition sit in VGPR lanes and are read with v_readlane (see
+// "register tables" below).
 //
 // Semantics are those of the host front end (host/vp8_parse.c, itself pinned to the reference m05:
 // src/m05_tokens/vp8_tokens.c:275-352, :354-622, :868-926): de-zigzagged coefficients, explicit
