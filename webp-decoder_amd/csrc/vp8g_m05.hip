@@ -355,6 +355,8 @@ DEV void tokens_wave(const Vp8gTokFrame& J, const uint8_t* pl, Out o, lds_u32* c
 	uint32_t vb[2];
 #pragma unroll
 	for (int k = 0; k < 2; k++) vb[k] = (L & 31u) < 24u ? cp[(2 * k + (L >> 5)) * 72 + (L & 31u) * 3 + 2] : 0u;
+	const TypeTab tt_y{va[PLANE_Y_AFTER_Y2], vb[0], 0}, tt_y2{va[PLANE_Y2], vb[0], 32}, tt_uv{va[PLANE_UV], vb[1], 0},
+	    tt_yalone{va[PLANE_Y_ALONE], vb[1], 32};
 	DBool tb;
 	dinit(tb, pl, 0, -8, 255u, J.part_off[w], J.part_end[w]);
 	dfill(tb, pl);
@@ -395,29 +397,19 @@ DEV void tokens_wave(const Vp8gTokFrame& J, const uint8_t* pl, Out o, lds_u32* c
 				left &= ~clr;
 				ab &= ~clr;
 			} else {
-				for (int k = has_y2 ? -1 : 0; k < 24; k++) {
-					uint32_t type, first, li, ai;
-					int16_t* dst;
-					if (k < 0) {
-						type = PLANE_Y2, first = 0, li = ai = 8;
-						dst = o.cy2 + mb * 16u;
-					} else if (k < 16) {
-						type = has_y2 ? PLANE_Y_AFTER_Y2 : PLANE_Y_ALONE, first = has_y2 ? 1u : 0u;
-						li = (uint32_t)k >> 2, ai = (uint32_t)k & 3u;
-						dst = o.cy + (mb * 16u + (uint32_t)k) * 16u;
-					} else {
-						const uint32_t j = (uint32_t)k - 16u, p = j >> 2, jj = j & 3u;
-						type = PLANE_UV, first = 0;
-						li = 4u + 2u * p + (jj >> 1), ai = 4u + 2u * p + (jj & 1u);
-						dst = (p ? o.cv : o.cu) + (mb * 4u + jj) * 16u;
-					}
-					const TypeTab tt{type == 0 ? va[0] : type == 1 ? va[1] : type == 2 ? va[2] : va[3],
-					                 type < 2 ? vb[0] : vb[1], (type & 1u) * 32u};
+				auto blk = [&](const TypeTab& tt, uint32_t first, uint32_t li, uint32_t ai, int16_t* dst) {
 					const uint32_t ctx = ((left >> li) & 1u) + ((ab >> ai) & 1u);
 					const bool nz = read_block(tb, pl, tt, first, ctx, dst);
 					any |= nz;
 					left = (left & ~(1u << li)) | ((uint32_t)nz << li);
 					ab = (ab & ~(1u << ai)) | ((uint32_t)nz << ai);
+				};
+				if (has_y2) blk(tt_y2, 0, 8, 8, o.cy2 + mb * 16u);
+				const TypeTab tty = has_y2 ? tt_y : tt_yalone;
+				for (uint32_t k = 0; k < 16u; k++) blk(tty, has_y2 ? 1u : 0u, k >> 2, k & 3u, o.cy + (mb * 16u + k) * 16u);
+				for (uint32_t j = 0; j < 8u; j++) {
+					const uint32_t p = j >> 2, jj = j & 3u;
+					blk(tt_uv, 0, 4u + 2u * p + (jj >> 1), 4u + 2u * p + (jj & 1u), (p ? o.cv : o.cu) + (mb * 4u + jj) * 16u);
 				}
 			}
 			if (L == 0) {
