@@ -405,8 +405,11 @@ DEV void tokens_wave(const Vp8gTokFrame& J, const uint8_t* pl, Out o, lds_u32* c
 					ab = (ab & ~(1u << ai)) | ((uint32_t)nz << ai);
 				};
 				if (has_y2) blk(tt_y2, 0, 8, 8, o.cy2 + mb * 16u);
-				const TypeTab tty = has_y2 ? tt_y : tt_yalone;
-				for (uint32_t k = 0; k < 16u; k++) blk(tty, has_y2 ? 1u : 0u, k >> 2, k & 3u, o.cy + (mb * 16u + k) * 16u);
+				if (has_y2) {  // two loops: the table and the first position are constants in each
+					for (uint32_t k = 0; k < 16u; k++) blk(tt_y, 1u, k >> 2, k & 3u, o.cy + (mb * 16u + k) * 16u);
+				} else {
+					for (uint32_t k = 0; k < 16u; k++) blk(tt_yalone, 0u, k >> 2, k & 3u, o.cy + (mb * 16u + k) * 16u);
+				}
 				for (uint32_t j = 0; j < 8u; j++) {
 					const uint32_t p = j >> 2, jj = j & 3u;
 					blk(tt_uv, 0, 4u + 2u * p + (jj >> 1), 4u + 2u * p + (jj & 1u), (p ? o.cv : o.cu) + (mb * 4u + jj) * 16u);
