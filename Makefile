@@ -15,7 +15,8 @@ OFFLOAD_ARCH ?= gfx950
 
 HOST_SRC := $(PKG)/host/webp_riff.c $(PKG)/host/vp8_parse.c $(PKG)/host/vp8_synth.c
 HOST_HDR := $(PKG)/host/vp8_front.h $(PKG)/host/vp8_bool.h $(PKG)/host/vp8_tables.inc include/vp8g.h
-HIP_SRC := $(PKG)/csrc/vp8g_kernels.hip $(PKG)/csrc/vp8g_shim.hip $(PKG)/csrc/vp8g_rgb.hip $(PKG)/csrc/vp8g_pipeline.hip $(PKG)/csrc/vp8g_m05.hip
+HIP_SRC := $(PKG)/csrc/vp8g_kernels.hip $(PKG)/csrc/vp8g_shim.hip $(PKG)/csrc/vp8g_rgb.hip $(PKG)/csrc/vp8g_pipeline.hip $(PKG)/csrc/vp8g_m05.hip \
+	$(PKG)/csrc/vp8g_digest.hip
 HIP_HDR := $(PKG)/csrc/vp8g_device.h include/vp8g.h $(PKG)/host/vp8_front.h
 # libvp8g links the host front end (the end-to-end batch path runs m05 on worker threads)
 HIP_LINK := -L$(LIB) -lvp8host -Wl,-rpath,'$$ORIGIN' -lpthread
@@ -24,7 +25,10 @@ CFLAGS := -std=c11 -O3 -march=x86-64-v3 -Wall -Wextra -Wpedantic -fPIC -D_POSIX_
 HIPFLAGS := -std=c++17 -O3 --offload-arch=$(OFFLOAD_ARCH) -fPIC -Wall -Wno-unused-function \
 	-fvisibility=hidden -I include -munsafe-fp-atomics
 
-all: lib oracle
+all: lib oracle $(LIB)/diag/libvp8g_stall.so
+
+# (oracle/ re-links the reference CLI against libvp8g.so: build the library first)
+oracle: lib
 
 lib: $(LIB)/libvp8host.so $(LIB)/libvp8g.so $(BIN)/decoder
 
@@ -47,11 +51,15 @@ oracle:
 # per-phase shader-clock stamps, and phase ablations (timing only, wrong output).
 DIAG := $(LIB)/diag
 DIAG_VARIANTS := stamps abl1 abl2 abl4 abl8 abl15
-diag: $(foreach v,$(DIAG_VARIANTS),$(DIAG)/libvp8g_$(v).so)
+diag: $(foreach v,$(DIAG_VARIANTS),$(DIAG)/libvp8g_$(v).so) $(DIAG)/libvp8g_stall.so
 $(DIAG):
 	mkdir -p $@
 $(DIAG)/libvp8g_stamps.so: $(HIP_SRC) $(HIP_HDR) | $(DIAG)
 	$(HIPCC) $(HIPFLAGS) -DVP8G_STAMPS -shared -Wl,-Bsymbolic -o $@ $(HIP_SRC) -L$(LIB) -lvp8host -Wl,-rpath,'$$ORIGIN/..' -lpthread
+# test build: wave 1 of every frame never publishes its progress and a wait gives up after 20 ms
+# (tests/test_gpu_batch.py: a stalled producer must end the launch promptly with EIO)
+$(DIAG)/libvp8g_stall.so: $(HIP_SRC) $(HIP_HDR) | $(DIAG)
+	$(HIPCC) $(HIPFLAGS) -DVP8G_WAIT_TICKS=2000000ull -DVP8G_TEST_STALL_WAVE=1 -shared -Wl,-Bsymbolic -o $@ $(HIP_SRC) -L$(LIB) -lvp8host -Wl,-rpath,'$$ORIGIN/..' -lpthread
 $(DIAG)/libvp8g_abl%.so: $(HIP_SRC) $(HIP_HDR) | $(DIAG)
 	$(HIPCC) $(HIPFLAGS) -DVP8G_ABLATE=$* -shared -Wl,-Bsymbolic -o $@ $(HIP_SRC) -L$(LIB) -lvp8host -Wl,-rpath,'$$ORIGIN/..' -lpthread
 

@@ -202,6 +202,15 @@ int vp8g_decode_batch_device(const Vp8gFrameDesc* h_descs, const Vp8gFrameDesc* 
                              const Vp8gBatchArrays* arrays, uint8_t* d_out, void* hip_stream,
                              uint32_t waves_per_frame);
 
+/* Per-frame 64-bit digests of a device-resident batch's outputs (parity without copying pixels
+ * back): d_digests[i] = digest of frame i's cropped I420 bytes (Y, U, V at stride = row width, the
+ * file the reference CLI writes): D = L*K + sum_i mix(w_i + (i+1)*K) mod 2^64 over the bytes as
+ * little-endian u64 words w_i (last one zero-padded), K = 0x9E3779B97F4A7C15, mix = splitmix64's
+ * finaliser.  Descriptors must have the contiguous layout vp8g_make_frame_desc
+ * builds (else EINVAL).  Asynchronous on `hip_stream`; 0 or -1 + errno. */
+int vp8g_frame_digests(const Vp8gFrameDesc* h_descs, const Vp8gFrameDesc* d_descs, uint32_t n_frames,
+                       const uint8_t* d_out, uint64_t* d_digests, void* hip_stream);
+
 /* Host-side batch: upload n decoded frames, run one launch, download into n freshly
  * yuv420_alloc()ed images.  Returns 0 / -1+errno (EIO on a HIP failure). */
 int vp8g_reconstruct_batch(const Vp8KeyFrameHeader* const* kfs, const Vp8DecodedFrame* const* frames, uint32_t n,

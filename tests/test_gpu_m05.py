@@ -143,3 +143,22 @@ def test_pipeline_multi_partition(vp8g, manifest, device_m05):
     outs, st = vp8g.gpu_decode_webp_batch(files[:3] + [(FIXTURES / rels[0]).read_bytes()], True, 4,
                                           device_m05=device_m05)
     assert all(s != 0 for s in st[:3]) and st[3] == 0
+
+
+@pytest.mark.parametrize("device_m05", [False, True], ids=["host_m05", "device_m05"])
+@pytest.mark.parametrize("filtered,key", [(False, "yuv"), (True, "yuvf")])
+def test_libwebp_multi_partition_streams(vp8g, device_m05, filtered, key):
+    """genuine 2/4/8-partition streams encoded by libwebp 1.2.2 (tests/fixtures_mp/,
+    tools/make_big_fixtures.c) decode to libwebp's own I420 (tests/golden/multipart.json) in both
+    batch modes; the reference rejects these streams (src/m05_tokens/vp8_tokens.c:357-360)."""
+    import json
+    mp = json.loads((ROOT / "tests" / "golden" / "multipart.json").read_text())
+    names = sorted(mp["files"])
+    files = [(ROOT / "tests" / "fixtures_mp" / n).read_bytes() for n in names]
+    outs, st = vp8g.gpu_decode_webp_batch(files, filtered, 8, device_m05=device_m05, multi_partition=True)
+    assert st == [0] * len(names)
+    bad = [n for n, o in zip(names, outs) if sha(o) != mp["files"][n][key + "_sha256"]]
+    assert not bad, bad
+    gm = vp8g.gpu_m05(files, multi_partition=True)  # device m05 arrays: one token wave per partition
+    for n, g in zip(names, gm):
+        assert int(g["ymode"].size) == ((mp["files"][n]["width"] + 15) // 16) * ((mp["files"][n]["height"] + 15) // 16)

@@ -23,12 +23,12 @@ def sha(b):
 
 def test_manifest_covers_reference_corpus(manifest):
     # the reference m6/m7 gate glob (scripts/m7_compare_yuv_filtered_with_oracle.sh:29) = 429 files,
-    # plus the 4 penguins and our 8 large libwebp-encoded frames
+    # plus the 4 penguins and our 10 large libwebp-encoded frames
     files = manifest["files"]
     assert sum(1 for k in files if k.split("/")[0] in ("webp", "testimages", "generated")) == 429
     assert sum(1 for k in files if k.startswith("commons/")) == 4
-    assert sum(1 for k in files if k.startswith("big/")) == 8
-    assert manifest["libwebp_agreement"] == {"yuv": "441/441", "yuvf": "441/441", "rgb": "441/441", "png_out": "90/90"}
+    assert sum(1 for k in files if k.startswith("big/")) == 10
+    assert manifest["libwebp_agreement"] == {"yuv": "443/443", "yuvf": "443/443", "rgb": "443/443", "png_out": "90/90"}
 
 
 def test_oracle_and_front_end_vs_manifest(vp8g, manifest):

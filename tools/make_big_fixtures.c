@@ -8,7 +8,7 @@
  * (images/commons/penguin-q80.webp, decoded with libwebp), mirrored/tiled to the target size
  * with a per-variant offset, plus a smooth gradient overlay so variants differ.
  *
- *   make_big_fixtures <penguin.webp> <out_dir>
+ *   make_big_fixtures <penguin.webp> <out_dir> [name,name,...]   (only the named variants)
  * Build: gcc -O2 -I/opt/conda/include tools/make_big_fixtures.c /usr/lib/x86_64-linux-gnu/libwebp.so.7
  */
 #include <stdio.h>
@@ -26,6 +26,7 @@ typedef struct {
 	int segments;  /* 1..4 */
 	float quality;
 	int ox, oy; /* content offset */
+	int partitions; /* log2 of the token partition count (libwebp WebPConfig.partitions, 0..3) */
 } Variant;
 
 static const Variant kVariants[] = {
@@ -37,6 +38,18 @@ static const Variant kVariants[] = {
     {"uhd_c_normal_sharp6_seg1", 3840, 2160, 0, 80, 6, 1, 60.f, 1000, 200},
     {"uhd_d_normal_q90", 3840, 2160, 0, 30, 2, 4, 90.f, 1500, 1600},
     {"odd_1917x1083_normal", 1917, 1083, 0, 70, 1, 4, 50.f, 300, 900},
+    /* round 2: two more 1080p frames for the 1080p batch (bench --workload fhd4) */
+    {"fhd_c_normal_q85_seg4", 1920, 1080, 0, 40, 0, 4, 85.f, 700, 500},
+    {"fhd_d_normal_sharp2_seg1", 1920, 1080, 0, 70, 2, 1, 60.f, 1300, 100},
+    /* multi-partition token streams (2/4/8 partitions; the reference rejects them, ENOTSUP at
+     * src/m05_tokens/vp8_tokens.c:357-360): tests/fixtures_mp/, pinned by libwebp's decode */
+    {"mp2_fhd_normal", 1920, 1080, 0, 60, 0, 4, 75.f, 100, 200, 1},
+    {"mp4_fhd_simple_sharp3", 1920, 1080, 1, 50, 3, 4, 70.f, 400, 50, 2},
+    {"mp8_fhd_normal_seg1", 1920, 1080, 0, 55, 4, 1, 80.f, 900, 600, 3},
+    {"mp2_uhd_normal_seg4", 3840, 2160, 0, 60, 0, 4, 75.f, 250, 350, 1},
+    {"mp4_uhd_normal_q90", 3840, 2160, 0, 30, 2, 4, 90.f, 1200, 1400, 2},
+    {"mp8_uhd_simple", 3840, 2160, 1, 45, 1, 4, 75.f, 600, 800, 3},
+    {"mp8_odd_333x197_normal", 333, 197, 0, 70, 1, 4, 50.f, 30, 90, 3},
 };
 
 static int mirror(int v, int n) {
@@ -47,8 +60,8 @@ static int mirror(int v, int n) {
 }
 
 int main(int argc, char** argv) {
-	if (argc != 3) {
-		fprintf(stderr, "usage: make_big_fixtures <penguin.webp> <out_dir>\n");
+	if (argc != 3 && argc != 4) {
+		fprintf(stderr, "usage: make_big_fixtures <penguin.webp> <out_dir> [name,name,...]\n");
 		return 2;
 	}
 	FILE* fp = fopen(argv[1], "rb");
@@ -64,6 +77,13 @@ int main(int argc, char** argv) {
 	if (!src) return 1;
 	for (size_t vi = 0; vi < sizeof(kVariants) / sizeof(kVariants[0]); vi++) {
 		const Variant* v = &kVariants[vi];
+		if (argc == 4) { /* only the named variants */
+			char want[1024];
+			snprintf(want, sizeof(want), ",%s,", argv[3]);
+			char key[128];
+			snprintf(key, sizeof(key), ",%s,", v->name);
+			if (!strstr(want, key)) continue;
+		}
 		uint8_t* rgb = malloc((size_t)v->w * v->h * 3);
 		for (int y = 0; y < v->h; y++) {
 			for (int x = 0; x < v->w; x++) {
@@ -86,7 +106,10 @@ int main(int argc, char** argv) {
 		cfg.filter_strength = v->strength;
 		cfg.filter_sharpness = v->sharpness;
 		cfg.segments = v->segments;
-		cfg.partitions = 0;
+		cfg.partitions = v->partitions;
+		/* libwebp 1.2.2 writes one partition whatever `partitions` says on its token-buffer path
+		 * (method >= 3 without low_memory); low_memory selects the path that honours it */
+		cfg.low_memory = v->partitions > 0;
 		cfg.autofilter = 0;
 		if (!WebPValidateConfig(&cfg)) return 1;
 		pic.width = v->w;

@@ -53,6 +53,15 @@ constexpr int kPrioTab[11] = {VP8G_PRIO_TABLE, VP8G_PRIO_LF, VP8G_PRIO_WHT};
 #ifndef VP8G_ABLATE
 #define VP8G_ABLATE 0
 #endif
+// Bound of one dependency wait in s_memrealtime ticks (100 MHz): 2 s.  Test builds shorten it and
+// make one wave never publish its progress (VP8G_TEST_STALL_WAVE) to check that a stalled producer
+// ends the launch promptly with VP8G_ERR_TIMEOUT (tests/test_gpu_batch.py).
+#ifndef VP8G_WAIT_TICKS
+#define VP8G_WAIT_TICKS 200000000ull
+#endif
+#ifndef VP8G_TEST_STALL_WAVE
+#define VP8G_TEST_STALL_WAVE (-1)
+#endif
 #ifdef VP8G_STAMPS
 __device__ unsigned long long g_vp8g_stamps[16];
 __device__ unsigned long long g_vp8g_wave_times[64];  // frame 0: per wave {start, end} s_memrealtime
@@ -553,6 +562,9 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 		return p;
 	};
 
+	// Set once a dependency wait has timed out: the wave finishes without waiting again (its output
+	// is garbage and the status word says so), so a stalled producer costs one bound, not one per step.
+	bool dead = false;
 	for (uint32_t k = gw; k < npairs; k += GW) {
 		const bool xin = kS && wave == 0 && k > 0;             // predecessor pair in another part
 		const bool xout = kS && wave == NW - 1 && k + 1 < npairs;  // successor pair in another part
@@ -722,7 +734,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 
 			// ---------------------------------------------- wait: pair k-1's lower row 2 cols ahead
 			PRIO(1);
-			if (k > 0 && !(VP8G_ABLATE & 8)) {
+			if (k > 0 && !dead && !(VP8G_ABLATE & 8)) {
 				// (one column more lag across parts: the mailbox is read a step ahead of use)
 				const uint32_t lag = xin ? 5u : 4u;
 				const uint32_t need = (k - 1) * CP2 + ((t + lag < CP2) ? t + lag : CP2);
@@ -735,8 +747,9 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					if ((++spins & 1023u) == 0) {
 						const uint64_t now = __builtin_amdgcn_s_memrealtime();
 						if (t0 == 0) t0 = now;
-						else if (now - t0 > 200000000ull) {  // 2 s at 100 MHz: give up, flag it
+						else if (now - t0 > (uint64_t)VP8G_WAIT_TICKS) {  // give up, flag it, and never wait again
 							if (lane == 0) atomicOr(A.status, VP8G_ERR_TIMEOUT);
+							dead = true;
 							break;
 						}
 					}
@@ -1107,7 +1120,8 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 				if (lane == 0) __hip_atomic_store(gp_out, k * CP2 + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 			}
-			if (lane == 0) __hip_atomic_store(prog + wave, k * CP2 + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+			if (lane == 0 && wave != VP8G_TEST_STALL_WAVE)
+				__hip_atomic_store(prog + wave, k * CP2 + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 			STAMP(7);
 		}
 	}

@@ -287,13 +287,14 @@ DEV void modes_wave(const Vp8gTokFrame& J, const uint8_t* pl, Out o, lds_u32* ct
 	const uint32_t seg_probs = *(const uint32_t*)J.seg_probs;
 	DBool hb;
 	dinit(hb, pl, J.b_value, J.b_bits, J.b_range, J.b_next, J.p0_end);
-	uint32_t m = 0, cons = 0;
+	uint32_t m = 0, cons = 0, maxp = kMaxPolls;
 	for (uint32_t r = 0; r < rows; r++) {
 		uint32_t left_b = 0;  // right column's sub-block modes, 4 nibbles
 		for (uint32_t c = 0; c < cols; c++, m++) {
 			for (uint32_t polls = 0; m - cons >= kRing; polls++) {
-				if (polls == kMaxPolls) {
-					timeout(o);
+				if (polls >= maxp) {  // sticky: after one timeout the wave never waits again
+					if (maxp) timeout(o);
+					maxp = 0;
 					break;
 				}
 				__builtin_amdgcn_s_sleep(2);
@@ -361,14 +362,15 @@ DEV void tokens_wave(const Vp8gTokFrame& J, const uint8_t* pl, Out o, lds_u32* c
 	dinit(tb, pl, 0, -8, 255u, J.part_off[w], J.part_end[w]);
 	dfill(tb, pl);
 	const uint32_t prev = (w + nparts - 1u) % nparts;  // the wave of row r - 1
-	uint32_t prod = 0, up = 0;
+	uint32_t prod = 0, up = 0, maxp = kMaxPolls;
 	for (uint32_t r = w; r < rows; r += nparts) {
 		uint32_t left = 0;  // token contexts, bits as in above[]
 		for (uint32_t c = 0; c < cols; c++) {
 			const uint32_t m = r * cols + c;
 			for (uint32_t polls = 0; m >= prod; polls++) {
-				if (polls == kMaxPolls) {
-					timeout(o);
+				if (polls >= maxp) {
+					if (maxp) timeout(o);
+					maxp = 0;
 					prod = m + 1u;
 					break;
 				}
@@ -377,8 +379,9 @@ DEV void tokens_wave(const Vp8gTokFrame& J, const uint8_t* pl, Out o, lds_u32* c
 			}
 			if (nparts > 1 && r > 0) {  // row wavefront: MB (r - 1, c) done
 				for (uint32_t polls = 0; up < m - cols + 1u; polls++) {
-					if (polls == kMaxPolls) {
-						timeout(o);
+					if (polls >= maxp) {
+						if (maxp) timeout(o);
+						maxp = 0;
 						up = m;
 						break;
 					}

@@ -165,6 +165,26 @@ def i420_size(w: int, h: int) -> int:
     return w * h + 2 * ((w + 1) // 2) * ((h + 1) // 2)
 
 
+_DIG_K = np.uint64(0x9E3779B97F4A7C15)
+
+
+def digest64(buf) -> int:
+    """Digest of a byte string as vp8g_frame_digests computes it on the device (include/vp8g.h):
+    L*K + sum_i mix(w_i + (i+1)*K) mod 2^64 over little-endian u64 words (last zero-padded),
+    mix = splitmix64's finaliser.  Returned as an unsigned Python int."""
+    b = np.frombuffer(buf, dtype=np.uint8) if not isinstance(buf, np.ndarray) else buf.view(np.uint8).reshape(-1)
+    n = b.size
+    pad = (-n) % 8
+    if pad:
+        b = np.concatenate([b, np.zeros(pad, np.uint8)])
+    w = b.view("<u8")
+    z = w + (np.arange(1, w.size + 1, dtype=np.uint64) * _DIG_K)
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    z ^= z >> np.uint64(31)
+    return (n * 0x9E3779B97F4A7C15 + int(z.sum(dtype=np.uint64))) & 0xFFFFFFFFFFFFFFFF
+
+
 _libs: dict = {}
 
 
@@ -219,6 +239,8 @@ def gpu_lib():
         lib.vp8g_i420_size.restype = C.c_uint64
         lib.vp8g_decode_batch_device.argtypes = [P(Vp8gFrameDesc), C.c_void_p, C.c_uint32, P(Vp8gBatchArrays),
                                                  C.c_void_p, C.c_void_p, C.c_uint32]
+        lib.vp8g_frame_digests.argtypes = [P(Vp8gFrameDesc), C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
+                                           C.c_void_p]
         lib.vp8g_reconstruct_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int, P(Yuv420Image)]
         lib.vp8g_last_error.restype = C.c_char_p
         lib.vp8g_abi_version.restype = C.c_uint32
