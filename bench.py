@@ -274,7 +274,14 @@ def run_workload(name, args, rank, world, dist, dev, golden, rank_factory=Rank):
     import vp8g_dist
     r = rank_factory(name, args, rank, world, dev, golden, dist)
     stream = torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else 0
-    elapsed, kern = timed(lambda: r.batch.launch(stream, args.waves), args.steps, args.warmup, dist, dev)
+    lib = vp8g.gpu_lib() if dev.type == "cuda" else None
+    stamps = lib is not None and hasattr(lib, "vp8g_debug_stamps")  # diagnostic build (VP8G_STAMPS) only
+    if stamps:
+        for _ in range(args.warmup):
+            r.batch.launch(stream, args.waves)
+        sync(dev)
+        lib.vp8g_debug_stamps((C.c_ulonglong * 16)(), 1)
+    elapsed, kern = timed(lambda: r.batch.launch(stream, args.waves), args.steps, 0 if stamps else args.warmup, dist, dev)
     status = r.batch.status_word()
     dig = r.batch.digests(stream)
     # every rank's digests reach rank 0 (64 bits per frame, never pixels); rank 0 checks each one
@@ -313,6 +320,13 @@ def run_workload(name, args, rank, world, dist, dev, golden, rank_factory=Rank):
         "cpu_baseline": None,
         "_rank": r,
     }
+    if stamps:
+        acc = (C.c_ulonglong * 16)()
+        lib.vp8g_debug_stamps(acc, 1)
+        tot = sum(acc[:8]) or 1
+        names = ["residual+loads", "dep_wait", "borders", "recon", "save_ctx", "loopfilter", "store", "publish"]
+        obj["stamps"] = {k: round(acc[i] / tot, 4) for i, k in enumerate(names)}
+        obj["stamps"]["cycles_per_mb_per_wave"] = round(tot / (r.batch.total_mb * args.steps), 1)
     if name == "uhd4" and TRAFFIC_FILE.exists():
         tj = json.loads(TRAFFIC_FILE.read_text())
         if tj.get("frames") == r.n and tj.get("filtered") == r.filtered:
@@ -534,6 +548,8 @@ def main(argv=None):
             line["encode"] = enc_obj
         if e2e:
             line["end_to_end"] = e2e
+        if "stamps" in head:
+            line["stamps"] = head["stamps"]
         if not ok:
             line["parity_failure"] = True
         print(json.dumps(line), flush=True)

@@ -13,6 +13,6 @@ for grp in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_V
            "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU_INT32 SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE" \
            "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $R/$OUT/pmc$i -o pmc -- python3 $R/bench.py --no-cpu-baseline "$@" > $R/$OUT/pmc$i.log 2>&1 || { echo "pmc pass $i failed rc=$?"; exit 1; }
+  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $R/$OUT/pmc$i -o pmc -- python3 $R/bench.py "$@" > $R/$OUT/pmc$i.log 2>&1 || { echo "pmc pass $i failed rc=$?"; exit 1; }
 done
 echo pmc_done

@@ -250,6 +250,18 @@ DEV uint64_t vsel(bool c, uint64_t a, uint64_t b) {
 	asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(hi) : "v"((uint32_t)(b >> 32)), "v"((uint32_t)(a >> 32)), "s"(mk));
 	return ((uint64_t)hi << 32) | lo;
 }
+// Output stores through buffer resources.  A lane with nothing to store this round passes
+// kNoStore, an offset past the end of the plane, and the hardware's range check drops it: the
+// store instructions of a step are then issued on every path.  (Stores behind a branch would make
+// the compiler's vmcnt bookkeeping assume a path without stores, and the next step's wait for its
+// prefetched coefficients -- loaded before these stores -- would also wait for every store of this
+// step to be acknowledged: a full drain of the store queue per step, ~10 % of the kernel time.)
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+constexpr uint32_t kNoStore = 0x80000000u;
+DEV Rsrc plane_rsrc(uint8_t* base, uint32_t bytes) { return __builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)bytes, 0x00020000); }
+DEV void bst128(Rsrc r, uint32_t off, u32x4 v) { __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, 0); }
+DEV void bst64(Rsrc r, uint32_t off, u32x2 v) { __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)off, 0, 0); }
+
 // single-byte LDS access that the load/store vectoriser leaves alone
 DEV int ldb(const uint8_t* p) { return (int)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT); }
 DEV void stb(uint8_t* p, int v) { __hip_atomic_store(p, (uint8_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT); }
@@ -523,6 +535,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 	const uint32_t sy = D.stride_y, suv = D.stride_uv;
 	const uint32_t vofs = (uint32_t)(D.out_v - D.out_u);  // V plane relative to U (< 2^32 by construction)
 	const uint32_t yal = (uint32_t)(uintptr_t)outY, ual = (uint32_t)(uintptr_t)outU;  // alignment tests
+	const Rsrc rY = plane_rsrc(outY, sy * H), rC = plane_rsrc(outU, vofs + suv * CH);  // output planes
 	uint32_t* const prog = (uint32_t*)(smem + kProgress);
 	Ctx<kG> ctx;
 	ctx.lds = smem + kHdrBytes + NW * kWaveBytes;
@@ -612,7 +625,15 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			          (((yal + fl_offY) & 15u) == 0 ? 4u : 0u) | (row_ok && ln < 24 && prowC < CH ? 8u : 0u) |
 			          (kc >= 8 && nlast ? 16u : 0u) | (((ual + fl_offC) & 7u) == 0 ? 32u : 0u);
 		}
-		Pref nxt = prefetch(lane0, cbase, sbase, csh, 0);
+		// The step's 32 bytes per lane, loaded one step ahead.  One variable carried around the loop
+		// and reloaded right after its last use (the dequantisation), so no register copy -- which
+		// would have to wait for the loads to land -- sits at the end of the step.
+		Pref cur = prefetch(lane0, cbase, sbase, csh, 0);
+		// two dropped stores (kNoStore): the loop entry then has as many vector-memory operations
+		// after the prefetch as every step has (its two output stores), so the first use of the
+		// prefetched data waits for the loads alone, never for stores (see kNoStore)
+		bst128(rY, kNoStore, u32x4{0u, 0u, 0u, 0u});
+		bst64(rC, kNoStore, u32x2{0u, 0u});
 
 		for (uint32_t t = 0; t < T; t++) {
 			// Lane-derived values are recomputed every step from a laundered lane id: hoisting the
@@ -632,9 +653,6 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			uint8_t* const abUV = hv + kAbUV;
 			uint8_t* const left = hv + kLeft;
 
-			const Pref cur = nxt;
-			nxt = prefetch(lane, cbase, sbase, csh, (int)t + 1);
-
 			// per-half side info (lanes 26..29 / 58..61 hold it)
 			// per-half side info, held by lanes 26..29 / 58..61: fetched with ds_bpermute (LDS
 			// crossbar, no LDS memory) instead of readlane + per-half select
@@ -645,6 +663,12 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			const int hasc = __builtin_amdgcn_ds_bpermute(sdl + 12, (int)cur.side);
 			const bool bpred = ymode == 4;
 			const uint32_t y0 = r * 16, cy0 = r * 8, x0 = cu * 16, cx0 = cu * 8;
+			// the half's 16 B_PRED modes, from lane 25 / 57 (used by the B_PRED phase)
+			const int bml = (hh ? 57 : 25) * 4;
+			const u32x4 bmw = u32x4{(uint32_t)__builtin_amdgcn_ds_bpermute(bml, (int)cur.a.x),
+			                        (uint32_t)__builtin_amdgcn_ds_bpermute(bml, (int)cur.a.y),
+			                        (uint32_t)__builtin_amdgcn_ds_bpermute(bml, (int)cur.a.z),
+			                        (uint32_t)__builtin_amdgcn_ds_bpermute(bml, (int)cur.a.w)};
 
 			// ---------------------------------------------- residual (no spatial dependency)
 			PRIO(0);
@@ -730,6 +754,9 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					st128(rp + 16, u32x4{rs[4], rs[5], rs[6], rs[7]});
 				}
 			}
+			// next step's coefficients into the same registers (the dequantisation above was cur's last
+			// use; one definition on every path, so the loop carries it without copies)
+			cur = prefetch(lane, cbase, sbase, csh, (int)t + 1);
 			STAMP(0);
 
 			// ---------------------------------------------- wait: pair k-1's lower row 2 cols ahead
@@ -911,11 +938,6 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					// last sub-block column come from the MB above (abY + 32), the left column of
 					// sub-block column j is at kLeft - 16 j (kColY, written here by the lanes of
 					// pixel column 3), P is the byte before the above row (i == 0) or the left column.
-					const int bml = (hh ? 57 : 25) * 4;  // the half's mode list, from lane 25 / 57
-					const u32x4 bmw = u32x4{(uint32_t)__builtin_amdgcn_ds_bpermute(bml, (int)cur.a.x),
-					                        (uint32_t)__builtin_amdgcn_ds_bpermute(bml, (int)cur.a.y),
-					                        (uint32_t)__builtin_amdgcn_ds_bpermute(bml, (int)cur.a.z),
-					                        (uint32_t)__builtin_amdgcn_ds_bpermute(bml, (int)cur.a.w)};
 					const int g = (ln >> 4) & 1, p = ln & 15, rr = p >> 2, cc = p & 3;
 					uint8_t* const tpix = tY + slot * 16 + 4 * kTP + kBS * g + kTP * rr + cc;  // + kBS i0 + 4 s
 					const uint8_t* const tA = tY + slot * 16 + 3 * kTP + kBS * g;             // + kBS i0 + 4 s
@@ -1000,7 +1022,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 				const uint32_t off = __umul24(prow, sy) + colpx;
 				const bool vis = ok && prow < H && !(VP8G_ABLATE & 4);
 				const bool full = colpx + 16u <= W && ((yal + off) & 15u) == 0;
-				if (vis && full) *(u32x4*)(outY + off) = u32x4{lo.x, lo.y, hi.x, hi.y};
+				bst128(rY, vis && full ? off : kNoStore, u32x4{lo.x, lo.y, hi.x, hi.y});
 				if (__ballot(vis && !full) != 0ull) {
 					if (vis && !full) {
 						const uint32_t n = W - colpx, cnt = n < 16u ? n : 16u;
@@ -1013,7 +1035,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 				const uint32_t off = (p ? vofs : 0u) + __umul24(prow, suv) + colpx;  // from outU
 				const bool vis = ok && prow < CH && !(VP8G_ABLATE & 4);
 				const bool full = colpx + 8u <= CW && ((ual + off) & 7u) == 0;
-				if (vis && full) *(u32x2*)(outU + off) = lo;
+				bst64(rC, vis && full ? off : kNoStore, lo);
 				if (__ballot(vis && !full) != 0ull) {
 					if (vis && !full) {
 						const uint32_t n = CW - colpx, cnt = n < 8u ? n : 8u;
@@ -1021,22 +1043,89 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					}
 				}
 			};
+			// This step's row piece of each lane for the two store rounds (luma 16 B, chroma 8 B):
+			// computed on either path, stored once after the join (see kNoStore).  A piece that is
+			// visible but cut by the right edge, or not aligned, goes byte by byte (rare branch).
+			uint32_t offY = kNoStore, offC = kNoStore, poffY = 0, poffC = 0, pcntY = 0, pcntC = 0;
+			u32x2 yl0, yl1, cl0;
+			const uint8_t* srcY;
+			const uint8_t* srcC;
 			if (!lf_on) {
-				// unfiltered: MB(r, c) is final as soon as it is reconstructed
-				if (ln < 16) {
-					const uint8_t* src = tY + (4 + ln) * kTP + slot * 16;
-					emitY(act, y0 + ln, cu, src, ld64(src), ld64(src + 8));
-				} else {
-					const int p = (ln - 16) >> 3, row = ln & 7;
-					const uint8_t* src = tC + p * 16 + (4 + row) * kTP + slot * 8;
-					emitC(act, p, cy0 + row, cu, src, ld64(src));
+				// unfiltered: MB(r, c) is final as soon as it is reconstructed; lanes 0..15 store luma
+				// rows, 16..31 chroma rows
+				const bool yl = ln < 16;
+				srcY = tY + (4 + (ln & 15)) * kTP + slot * 16;
+				const int p = (ln >> 3) & 1, row = ln & 7;
+				srcC = tC + p * 16 + (4 + row) * kTP + slot * 8;
+				yl0 = ld64(srcY), yl1 = ld64(srcY + 8), cl0 = ld64(srcC);
+				{
+					const uint32_t colpx = cu * 16u, prow = y0 + (uint32_t)(ln & 15);
+					const uint32_t off = __umul24(prow, sy) + colpx;
+					const bool vis = act && yl && prow < H && !(VP8G_ABLATE & 4);
+					const bool full = colpx + 16u <= W && ((yal + off) & 15u) == 0;
+					offY = vis && full ? off : kNoStore;
+					poffY = off, pcntY = vis && !full ? min(W - colpx, 16u) : 0u;
+				}
+				{
+					const uint32_t colpx = cu * 8u, prow = cy0 + (uint32_t)row;
+					const uint32_t off = (p ? vofs : 0u) + __umul24(prow, suv) + colpx;
+					const bool vis = act && !yl && prow < CH && !(VP8G_ABLATE & 4);
+					const bool full = colpx + 8u <= CW && ((ual + off) & 7u) == 0;
+					offC = vis && full ? off : kNoStore;
+					poffC = off, pcntC = vis && !full ? min(CW - colpx, 8u) : 0u;
 				}
 			} else {
+				{  // luma: ln 0..3 the MB above's bottom rows (this column, final now); 4..19 the left MB
+					const bool top = ln < 4;
+					const uint32_t col = top ? cu : cu - 1;
+					srcY = tY + ln * kTP + (top ? slot : slot ^ 1) * 16;
+					yl0 = ld64(srcY), yl1 = ld64(srcY + 8);
+					const bool ok = act && (fl_bits & 1u) && (top || c > 0);
+					const bool to_ctx = ok && (fl_bits & 2u);
+					if (to_ctx) ctx.wr128(lf_off(col) + (ln - 16) * 16, u32x4{yl0.x, yl0.y, yl1.x, yl1.y});
+#if VP8G_ABLATE & 16  // diagnostic: same stores, linearised per half (whole lines; output wrong)
+					const uint32_t linR = (H * sy) / (2 * NW) & ~1023u;
+					const uint32_t colpx = col * 16u, off = (uint32_t)(wave * 2 + hh) * linR + ((k * T + t) * 512u + (uint32_t)ln * 16u) % linR;
+#else
+					const uint32_t colpx = col * 16u, off = fl_offY + colpx;
+#endif
+					const bool vis = ok && !to_ctx && !(VP8G_ABLATE & 4);
+					const bool full = (fl_bits & 4u) && colpx + 16u <= W;
+					offY = vis && full ? off : kNoStore;
+					poffY = off, pcntY = vis && !full ? min(W - colpx, 16u) : 0u;
+				}
+				{  // chroma: plane ln / 12, tile row ln % 12 (same split)
+					const int p = ln >= 12 ? 1 : 0, kr = ln - 12 * p;
+					const bool top = kr < 4;
+					const uint32_t col = top ? cu : cu - 1;
+					srcC = tC + p * 16 + kr * kTP + (top ? slot : slot ^ 1) * 8;
+					cl0 = ld64(srcC);
+					const bool ok = act && (fl_bits & 8u) && (top || c > 0);
+					const bool to_ctx = ok && (fl_bits & 16u);
+					if (to_ctx) ctx.wr64(lf_off(col) + 64 + p * 32 + (kr - 8) * 8, cl0);
+#if VP8G_ABLATE & 16
+					const uint32_t linRc = (CH * suv) / (2 * NW) & ~1023u;
+					const uint32_t colpx = col * 8u, off = (uint32_t)(wave * 2 + hh) * linRc + ((k * T + t) * 256u + (uint32_t)ln * 8u) % linRc;
+#else
+					const uint32_t colpx = col * 8u, off = fl_offC + colpx;
+#endif
+					const bool vis = ok && !to_ctx && !(VP8G_ABLATE & 4);
+					const bool full = (fl_bits & 32u) && colpx + 8u <= CW;
+					offC = vis && full ? off : kNoStore;
+					poffC = off, pcntC = vis && !full ? min(CW - colpx, 8u) : 0u;
+				}
+			}
+			bst128(rY, offY, u32x4{yl0.x, yl0.y, yl1.x, yl1.y});
+			bst64(rC, offC, cl0);
+			if (__ballot(pcntY | pcntC) != 0ull) {
+				for (uint32_t q = 0; q < pcntY; q++) outY[poffY + q] = srcY[q];
+				for (uint32_t q = 0; q < pcntC; q++) outU[poffC + q] = srcC[q];
+			}
+			if (lf_on) {
 				const bool last_row = r + 1 == R;
 				// tile row t of a column holds image row (MB row origin) + t - 4; rows >= 16 (luma) /
 				// >= 8 (chroma) are the bottom 4 rows the next MB row still filters: to ctx_lf unless
 				// this is the last MB row
-				// (the row piece is loaded once, by every lane -- addresses stay inside the half's area)
 				auto flushY = [&](bool ok, int trow, uint32_t col, int sl) {
 					const uint8_t* src = tY + trow * kTP + sl * 16;
 					const u32x2 lo = ld64(src), hi = ld64(src + 8);
@@ -1051,45 +1140,6 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					if (to_ctx) ctx.wr64(lf_off(col) + 64 + p * 32 + (trow - 8) * 8, lo);
 					emitC(ok && !to_ctx, p, cy0 + trow - 4, col, src, lo);
 				};
-				{  // luma: ln 0..3 the MB above's bottom rows (this column, final now); 4..19 the left MB
-					const bool top = ln < 4;
-					const uint32_t col = top ? cu : cu - 1;
-					const uint8_t* src = tY + ln * kTP + (top ? slot : slot ^ 1) * 16;
-					const u32x2 lo = ld64(src), hi = ld64(src + 8);
-					const bool ok = act && (fl_bits & 1u) && (top || c > 0);
-					const bool to_ctx = ok && (fl_bits & 2u);
-					if (to_ctx) ctx.wr128(lf_off(col) + (ln - 16) * 16, u32x4{lo.x, lo.y, hi.x, hi.y});
-					const uint32_t colpx = col * 16u, off = fl_offY + colpx;
-					const bool vis = ok && !to_ctx && !(VP8G_ABLATE & 4);
-					const bool full = (fl_bits & 4u) && colpx + 16u <= W;
-					if (vis && full) *(u32x4*)(outY + off) = u32x4{lo.x, lo.y, hi.x, hi.y};
-					if (__ballot(vis && !full) != 0ull) {
-						if (vis && !full) {
-							const uint32_t n = W - colpx, cnt = n < 16u ? n : 16u;
-							for (uint32_t q = 0; q < cnt; q++) outY[off + q] = src[q];
-						}
-					}
-				}
-				{  // chroma: plane ln / 12, tile row ln % 12 (same split)
-					const int p = ln >= 12 ? 1 : 0, k = ln - 12 * p;
-					const bool top = k < 4;
-					const uint32_t col = top ? cu : cu - 1;
-					const uint8_t* src = tC + p * 16 + k * kTP + (top ? slot : slot ^ 1) * 8;
-					const u32x2 lo = ld64(src);
-					const bool ok = act && (fl_bits & 8u) && (top || c > 0);
-					const bool to_ctx = ok && (fl_bits & 16u);
-					if (to_ctx) ctx.wr64(lf_off(col) + 64 + p * 32 + (k - 8) * 8, lo);
-					const uint32_t colpx = col * 8u, off = fl_offC + colpx;
-					const bool vis = ok && !to_ctx && !(VP8G_ABLATE & 4);
-					const bool full = (fl_bits & 32u) && colpx + 8u <= CW;
-					if (vis && full) *(u32x2*)(outU + off) = lo;
-					if (__ballot(vis && !full) != 0ull) {
-						if (vis && !full) {
-							const uint32_t n = CW - colpx, cnt = n < 8u ? n : 8u;
-							for (uint32_t q = 0; q < cnt; q++) outU[off + q] = src[q];
-						}
-					}
-				}
 				SUBMARK(21);
 				if (__ballot(act && cu + 1 == C) != 0ull) {  // last column: its own rows are final too
 					const bool own = act && cu + 1 == C;
