@@ -129,3 +129,27 @@ def test_cli_end_to_end(manifest, tmp_path, rel, flag):
     assert r.returncode == 0, r.stderr
     key = "yuvf_sha256" if flag == "-yuvf" else "yuv_sha256"
     assert sha(out.read_bytes()) == manifest["files"][rel][key]
+
+
+def test_missing_segment_map_without_segmentation(vp8g):
+    """segment_id = NULL and a wrong mb_total are accepted when segmentation is off, as by the
+    reference (vp8_recon.c:447, vp8_loopfilter.c:169-171); output equals the oracle's on the frame
+    with an all-zero map."""
+    import ctypes as C
+    f = vp8g.synth_frame(333, 197, 21, 0)
+    ref = {}
+    fr = vp8g.Vp8DecodedFrame.from_buffer_copy(bytes(f.frame))
+    fr.segmentation_enabled = 0
+    g = vp8g.Frame(f.kf, fr)
+    g._alive = False  # arrays stay owned by f
+    for filtered in (False, True):
+        ref[filtered] = vp8g.oracle_reconstruct(g, filtered)
+    fr.segment_id = None
+    fr.mb_total = 7
+    lib = vp8g.gpu_lib()
+    for filtered in (False, True):
+        img = vp8g.Yuv420Image()
+        fn = lib.vp8_reconstruct_keyframe_yuv_filtered if filtered else lib.vp8_reconstruct_keyframe_yuv
+        assert fn(C.byref(f.kf), C.byref(fr), C.byref(img)) == 0
+        assert vp8g._image_bytes(img) == ref[filtered]
+        lib.yuv420_free(C.byref(img))

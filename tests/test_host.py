@@ -56,6 +56,24 @@ def test_null_arguments_fail_with_einval(vp8g):
     assert lib.yuv420_alloc(C.byref(img), 0, 5) == -1 and C.get_errno() == 22
 
 
+def test_segment_map_required_only_with_segmentation(vp8g):
+    """Like the reference (vp8_recon.c:447, vp8_loopfilter.c:169-171): segment_id is read only when
+    segmentation is enabled and mb_total is never read.  Without a GPU the accepted frame fails
+    later with EIO, the rejected one up front with EINVAL."""
+    lib = C.CDLL(str(vp8g.LIB_DIR / "libvp8g.so"), use_errno=True)
+    f = vp8g.synth_frame(48, 32, 3, 0)  # profile 0: segmentation enabled
+    seg = f.frame.segment_id
+    d = vp8g.Vp8gFrameDesc()
+    fr = vp8g.Vp8DecodedFrame.from_buffer_copy(bytes(f.frame))
+    fr.segment_id = None
+    C.set_errno(0)
+    assert lib.vp8g_make_frame_desc(C.byref(f.kf), C.byref(fr), 1, 0, 0, C.byref(d)) == -1 and C.get_errno() == 22
+    fr.segmentation_enabled = 0
+    fr.mb_total = 12345  # never read
+    assert lib.vp8g_make_frame_desc(C.byref(f.kf), C.byref(fr), 1, 0, 0, C.byref(d)) == 0
+    assert bool(seg)
+
+
 def test_loopfilter_size_mismatch_is_einval(vp8g):
     lib = C.CDLL(str(vp8g.LIB_DIR / "libvp8g.so"), use_errno=True)
     lib.yuv420_alloc.argtypes = [C.POINTER(vp8g.Yuv420Image), C.c_uint32, C.c_uint32]

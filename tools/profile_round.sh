@@ -11,9 +11,9 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o trace -- \
-  python3 $R/bench.py --no-cpu-baseline --e2e-frames 0 --steps 10 --warmup 3 > $OUT/trace_bench.log 2>&1 || { echo "trace pass failed rc=$?"; exit 1; }
+  python3 $R/bench.py --no-cpu-baseline --e2e-frames 0 --extra none --encode none --steps 10 --warmup 3 > $OUT/trace_bench.log 2>&1 || { echo "trace pass failed rc=$?"; exit 1; }
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 400 rocprofv3 --pmc $c --output-format csv -d $OUT/pmc_$c -o pmc -- \
-    python3 $R/bench.py --no-cpu-baseline --e2e-frames 0 --steps 2 --warmup 1 > $OUT/pmc_$c.log 2>&1 || { echo "pmc $c failed rc=$?"; exit 1; }
+    python3 $R/bench.py --no-cpu-baseline --e2e-frames 0 --extra none --encode none --steps 2 --warmup 1 > $OUT/pmc_$c.log 2>&1 || { echo "pmc $c failed rc=$?"; exit 1; }
 done
 echo profile_done

@@ -212,7 +212,18 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 		const long v = atol(e);
 		if (v > 0 && (uint64_t)v < chunk_frames) chunk_frames = (uint32_t)v;
 	}
-	const uint64_t chunk_mbs = tok ? kTokChunkMbs : kChunkMbs;
+	uint64_t chunk_mbs = tok ? kTokChunkMbs : kChunkMbs;
+	{
+		// two chunk slots of ~1.3 KB per MB each (+ payloads): keep both within ~3/8 of the free
+		// device memory, so a device shared with other work gets smaller chunks instead of a failed
+		// allocation (EIO for every frame)
+		size_t fr = 0, tot = 0;
+		if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr) {
+			const uint64_t cap = (uint64_t)fr / 8192u;  // = fr * 3/8 / (2 slots x 1.5 KB)
+			const uint64_t floor_mbs = 1u << 15;         // one 4K frame and change
+			if (cap < chunk_mbs) chunk_mbs = cap > floor_mbs ? cap : floor_mbs;
+		}
+	}
 	for (uint32_t i = 0; i < n; i++) memset(&outs[i], 0, sizeof(outs[i]));
 	if (!threads) threads = default_threads();
 	if (threads > n) threads = n;

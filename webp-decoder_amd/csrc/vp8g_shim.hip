@@ -89,11 +89,15 @@ int fill_loopfilter(const Vp8DecodedFrame* d, Vp8gFrameDesc* out) {
 	return any;
 }
 
+// The arrays the reference's m06/m07 read (vp8_recon.c:423-712, vp8_loopfilter.c:166-283): like the
+// reference, segment_id only when segmentation is enabled (a missing map reads as segment 0) and
+// has_coeff may be NULL; mb_total is never read (mb_cols * mb_rows sizes everything).
 bool frame_ok(const Vp8DecodedFrame* d) {
 	return d && d->mb_cols && d->mb_rows && d->mb_cols <= 1024 && d->mb_rows <= 1024 &&
-	       (uint64_t)d->mb_cols * d->mb_rows == d->mb_total && d->segment_id && d->ymode && d->uv_mode && d->bmode &&
-	       d->coeff_y2 && d->coeff_y && d->coeff_u && d->coeff_v;
+	       (d->segment_id || !d->segmentation_enabled) && d->ymode && d->uv_mode && d->bmode && d->coeff_y2 && d->coeff_y &&
+	       d->coeff_u && d->coeff_v;
 }
+inline uint64_t mb_count(const Vp8DecodedFrame* d) { return (uint64_t)d->mb_cols * d->mb_rows; }
 
 inline uint64_t align256(uint64_t x) { return (x + 255) & ~(uint64_t)255; }
 
@@ -283,7 +287,7 @@ VP8G_API int vp8g_make_frame_desc(const Vp8KeyFrameHeader* kf, const Vp8DecodedF
 int vp8g::make_desc(const Vp8KeyFrameHeader* kf, const Vp8DecodedFrame* d, int filtered, uint64_t mb_offset,
                     uint64_t out_offset, Vp8gFrameDesc* out, bool dense_coeffs) {
 	if (!out || !d || !d->mb_cols || !d->mb_rows || d->mb_cols > 1024 || d->mb_rows > 1024 ||
-	    (uint64_t)d->mb_cols * d->mb_rows != d->mb_total || (dense_coeffs && !frame_ok(d))) {
+	    (dense_coeffs && !frame_ok(d))) {
 		errno = EINVAL;
 		return -1;
 	}
@@ -333,7 +337,7 @@ VP8G_API int vp8g_reconstruct_batch(const Vp8KeyFrameHeader* const* kfs, const V
 			errno = EINVAL;
 			return -1;
 		}
-		mbs += frames[i]->mb_total;
+		mbs += mb_count(frames[i]);
 		outb = align256(outb + vp8g_i420_size(kfs[i]->width, kfs[i]->height));
 	}
 	for (uint32_t i = 0; i < n; i++) {
@@ -365,14 +369,15 @@ VP8G_API int vp8g_reconstruct_batch(const Vp8KeyFrameHeader* const* kfs, const V
 	uint8_t* in = g_dev.in;
 	for (uint32_t i = 0; i < n; i++) {
 		const Vp8DecodedFrame* d = frames[i];
-		const uint64_t o = descs[i].mb_offset, k = d->mb_total;
+		const uint64_t o = descs[i].mb_offset, k = mb_count(d);
 		TRY(hipMemcpyAsync(in + L.y + o * 512, d->coeff_y, k * 512, hipMemcpyHostToDevice, s), "H2D");
 		TRY(hipMemcpyAsync(in + L.u + o * 128, d->coeff_u, k * 128, hipMemcpyHostToDevice, s), "H2D");
 		TRY(hipMemcpyAsync(in + L.v + o * 128, d->coeff_v, k * 128, hipMemcpyHostToDevice, s), "H2D");
 		TRY(hipMemcpyAsync(in + L.y2 + o * 32, d->coeff_y2, k * 32, hipMemcpyHostToDevice, s), "H2D");
 		TRY(hipMemcpyAsync(in + L.ym + o, d->ymode, k, hipMemcpyHostToDevice, s), "H2D");
 		TRY(hipMemcpyAsync(in + L.uvm + o, d->uv_mode, k, hipMemcpyHostToDevice, s), "H2D");
-		TRY(hipMemcpyAsync(in + L.seg + o, d->segment_id, k, hipMemcpyHostToDevice, s), "H2D");
+		if (d->segment_id) TRY(hipMemcpyAsync(in + L.seg + o, d->segment_id, k, hipMemcpyHostToDevice, s), "H2D");
+		else TRY(hipMemsetAsync(in + L.seg + o, 0, k, s), "memset");
 		if (d->has_coeff) TRY(hipMemcpyAsync(in + L.hasc + o, d->has_coeff, k, hipMemcpyHostToDevice, s), "H2D");
 		else TRY(hipMemsetAsync(in + L.hasc + o, 0, k, s), "memset");
 		TRY(hipMemcpyAsync(in + L.bm + o * 16, d->bmode, k * 16, hipMemcpyHostToDevice, s), "H2D");
@@ -433,8 +438,7 @@ VP8G_API int vp8_loopfilter_apply_keyframe(Yuv420Image* img, const Vp8DecodedFra
 		return -1;
 	}
 	if (img->width != d->mb_cols * 16u || img->height != d->mb_rows * 16u || !img->y || !img->u || !img->v ||
-	    !d->ymode || !d->segment_id || (uint64_t)d->mb_cols * d->mb_rows != d->mb_total || d->mb_cols > 1024 ||
-	    d->mb_rows > 1024) {
+	    !d->ymode || (!d->segment_id && d->segmentation_enabled) || d->mb_cols > 1024 || d->mb_rows > 1024) {
 		errno = EINVAL;
 		return -1;
 	}
@@ -458,7 +462,7 @@ VP8G_API int vp8_loopfilter_apply_keyframe(Yuv420Image* img, const Vp8DecodedFra
 	desc.src_stride_y = desc.stride_y;
 	desc.src_stride_uv = desc.stride_uv;
 	std::vector<Vp8gFrameDesc> descs(1, desc);
-	const uint64_t k = d->mb_total;
+	const uint64_t k = mb_count(d);
 	std::lock_guard<std::mutex> lk(g_dev.mu);
 	HIP_TRY(dev_init(), "init");
 	const InLayout L = in_layout(k, frame_bytes);
@@ -469,7 +473,8 @@ VP8G_API int vp8_loopfilter_apply_keyframe(Yuv420Image* img, const Vp8DecodedFra
 	uint8_t* in = g_dev.in;
 	const uint32_t cw = img->width / 2, ch = img->height / 2;
 	HIP_TRY(hipMemcpyAsync(in + L.ym, d->ymode, k, hipMemcpyHostToDevice, s), "H2D");
-	HIP_TRY(hipMemcpyAsync(in + L.seg, d->segment_id, k, hipMemcpyHostToDevice, s), "H2D");
+	if (d->segment_id) HIP_TRY(hipMemcpyAsync(in + L.seg, d->segment_id, k, hipMemcpyHostToDevice, s), "H2D");
+	else HIP_TRY(hipMemsetAsync(in + L.seg, 0, k, s), "memset");
 	if (d->has_coeff) HIP_TRY(hipMemcpyAsync(in + L.hasc, d->has_coeff, k, hipMemcpyHostToDevice, s), "H2D");
 	else HIP_TRY(hipMemsetAsync(in + L.hasc, 0, k, s), "memset");
 	uint8_t* src = in + L.src;
