@@ -44,6 +44,7 @@ def main():
         lib = C.CDLL(str(pathlib.Path(path).resolve()), use_errno=True)
         lib.vp8g_decode_batch_device.argtypes = [C.POINTER(vp8g.Vp8gFrameDesc), C.c_void_p, C.c_uint32,
                                                  C.POINTER(vp8g.Vp8gBatchArrays), C.c_void_p, C.c_void_p, C.c_uint32]
+        lib.vp8g_last_error.restype = C.c_char_p
         lib.vp8g_frame_digests.argtypes = [C.POINTER(vp8g.Vp8gFrameDesc), C.c_void_p, C.c_uint32, C.c_void_p,
                                            C.c_void_p, C.c_void_p]
         libs.append((ent, lib, int(w or 0)))
@@ -51,7 +52,8 @@ def main():
     def launch(lib, waves):
         rc = lib.vp8g_decode_batch_device(b.h_descs, C.c_void_p(b.d_descs.data_ptr()), b.n, C.byref(b.c_arrays),
                                           C.c_void_p(b.out.data_ptr()), C.c_void_p(stream), waves)
-        assert rc == 0
+        if rc != 0:
+            raise RuntimeError(f"launch failed: {lib.vp8g_last_error()!r}")
 
     times = {e: [] for e, _, _ in libs}
     parity = {}
