@@ -162,3 +162,18 @@ def test_libwebp_multi_partition_streams(vp8g, device_m05, filtered, key):
     gm = vp8g.gpu_m05(files, multi_partition=True)  # device m05 arrays: one token wave per partition
     for n, g in zip(names, gm):
         assert int(g["ymode"].size) == ((mp["files"][n]["width"] + 15) // 16) * ((mp["files"][n]["height"] + 15) // 16)
+
+
+@pytest.mark.parametrize("hybrid", ["0", "1"], ids=["pure_device", "hybrid"])
+def test_pipeline_device_m05_hybrid_split(vp8g, manifest, monkeypatch, hybrid):
+    """in device-m05 mode the heaviest frames go to the host threads (packed path)
+    and the rest to the device m05 (plan_frames in vp8g_pipeline.hip; VP8G_HYBRID=0 = all on the
+    device).  Both schedules reproduce the reference's -yuvf output, in the callers' order."""
+    monkeypatch.setenv("VP8G_HYBRID", hybrid)
+    rels = ["big/uhd_d_normal_q90.webp", "big/uhd_a_normal_seg4.webp", "big/fhd_normal_sharp5.webp",
+            "big/uhd_b_simple_sharp3.webp"] * 6 + sorted(manifest["files"])[::40]
+    files = [(FIXTURES / r).read_bytes() for r in rels]
+    outs, st = vp8g.gpu_decode_webp_batch(files, True, 4, device_m05=True)
+    assert st == [0] * len(rels)
+    bad = [r for r, o in zip(rels, outs) if sha(o) != manifest["files"][r]["yuvf_sha256"]]
+    assert not bad, bad[:8]

@@ -22,6 +22,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <memory>
@@ -107,34 +108,37 @@ uint32_t default_threads() {
 	return h ? h : 1u;
 }
 
-// Frames handed from the workers to the device thread.
+// Frames handed from the workers to the device thread, in the order `order` (positions), each
+// either decoded on the host into the packed format or only header-parsed for device m05 (dev[i]).
 struct Feed {
 	const ByteSpan* files = nullptr;
 	uint32_t n = 0;
-	bool tok = false;  // device m05: workers fill tj instead of pk
+	std::vector<uint8_t> dev;       // frame i: m05 on the device (workers fill tj[i], else pk[i])
+	std::vector<uint32_t> order;    // position -> frame index
 	unsigned fflags = 0;  // front-end flags (VP8F_MULTI_PARTITION)
 	std::vector<Vp8gPackedFrame> pk;
 	std::vector<TokJob> tj;
 	std::vector<int> err;
 	std::unique_ptr<uint8_t[]> ready;
 	std::atomic<uint32_t> next{0};
-	uint32_t limit = 0;  // workers may start frames < limit (guarded by mu)
+	uint32_t limit = 0;  // workers may start positions < limit (guarded by mu)
 	bool abort = false;
 	std::mutex mu;
 	std::condition_variable cv_ready, cv_limit;
 
 	void work() {
 		for (;;) {
-			const uint32_t i = next.fetch_add(1);
-			if (i >= n) return;
+			const uint32_t pos = next.fetch_add(1);
+			if (pos >= n) return;
 			{
 				std::unique_lock<std::mutex> lk(mu);
-				cv_limit.wait(lk, [&] { return i < limit || abort; });
+				cv_limit.wait(lk, [&] { return pos < limit || abort; });
 				if (abort) return;
 			}
+			const uint32_t i = order[pos];
 			int stage = 0, e = 0;
 			if (!files[i].data) e = EINVAL;
-			else if (tok) {
+			else if (dev[i]) {
 				TokJob& j = tj[i];
 				if (vp8f_token_header_memory(files[i].data, files[i].size, &j.kf, &j.hdr, &j.tf, &j.poff, &j.psize, &stage,
 				                             fflags) != 0)
@@ -198,6 +202,47 @@ hipError_t grow(Slot& s, size_t need) {
 	return e;
 }
 
+// Which frames run m05 on the device and in which order the workers take them.  Without
+// VP8G_BATCH_DEVICE_M05 every frame is decoded on the host, in index order.  With it the device
+// runs m05 as one workgroup per frame, so a chunk lasts as long as its heaviest frame (per-frame
+// latency ~ kDevNsPerByte x payload bytes), while the host threads would otherwise only parse
+// headers: the heaviest frames go to the host threads (~ kHostNsPerByte x bytes each, `threads`
+// at a time) for as long as that keeps the host's share shorter than the device's
+// (VP8G_HYBRID=0 turns this off).  Device frames come first, so their chunks
+// launch while the host threads decode the heavy ones.
+constexpr double kDevNsPerByte = 850.0;   // device m05 latency, 4K fixtures
+constexpr double kHostNsPerByte = 35.0;   // host m05 into the packed format, one thread: effective value
+                                          // calibrated on the box (tools/hybrid_sweep.py, profiles/r02_hybrid.json)
+void plan_frames(const ByteSpan* files, uint32_t n, bool tok, uint32_t threads, std::vector<uint8_t>& dev,
+                 std::vector<uint32_t>& order) {
+	dev.assign(n, tok ? 1 : 0);
+	order.resize(n);
+	for (uint32_t i = 0; i < n; i++) order[i] = i;
+	const char* hv = getenv("VP8G_HYBRID");
+	if (!tok || (hv && atoi(hv) == 0)) return;
+	double dev_per_b = kDevNsPerByte, host_per_b = kHostNsPerByte;
+	if (const char* e = getenv("VP8G_DEV_NS_PER_BYTE")) dev_per_b = atof(e);    // calibration knobs
+	if (const char* e = getenv("VP8G_HOST_NS_PER_BYTE")) host_per_b = atof(e);
+	std::vector<uint32_t> by_size(order);
+	std::stable_sort(by_size.begin(), by_size.end(),
+	                 [&](uint32_t x, uint32_t y) { return files[x].size > files[y].size; });
+	double host_ns = 0;
+	const double thr = threads ? (double)threads : 1.0;
+	for (uint32_t k = 0; k < n; k++) {
+		const uint32_t f = by_size[k];
+		const double dev_ns = dev_per_b * (double)files[f].size;  // the heaviest frame still on the device
+		const double h = host_ns + host_per_b * (double)files[f].size / thr;
+		if (h > dev_ns) break;
+		host_ns = h;
+		dev[f] = 0;
+	}
+	uint32_t p = 0;
+	for (uint32_t i = 0; i < n; i++)
+		if (dev[i]) order[p++] = i;
+	for (uint32_t k = 0; k < n; k++)
+		if (!dev[by_size[k]]) order[p++] = by_size[k];
+}
+
 }  // namespace
 
 VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int filtered, uint32_t threads, uint32_t flags,
@@ -207,12 +252,13 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 		return -1;
 	}
 	const bool tok = (flags & VP8G_BATCH_DEVICE_M05) != 0;
-	uint32_t chunk_frames = tok ? kTokChunkFrames : kChunkFrames;
+	uint32_t chunk_frames_pk = kChunkFrames, chunk_frames_tok = kTokChunkFrames;
 	if (const char* e = getenv("VP8G_CHUNK_FRAMES")) {  // test knob: smaller chunks
 		const long v = atol(e);
-		if (v > 0 && (uint64_t)v < chunk_frames) chunk_frames = (uint32_t)v;
+		if (v > 0 && (uint64_t)v < chunk_frames_pk) chunk_frames_pk = (uint32_t)v;
+		if (v > 0 && (uint64_t)v < chunk_frames_tok) chunk_frames_tok = (uint32_t)v;
 	}
-	uint64_t chunk_mbs = tok ? kTokChunkMbs : kChunkMbs;
+	uint64_t chunk_mbs_tok = kTokChunkMbs, chunk_mbs_pk = kChunkMbs;
 	{
 		// two chunk slots of ~1.3 KB per MB each (+ payloads): keep both within ~3/8 of the free
 		// device memory, so a device shared with other work gets smaller chunks instead of a failed
@@ -221,7 +267,8 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 		if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr) {
 			const uint64_t cap = (uint64_t)fr / 8192u;  // = fr * 3/8 / (2 slots x 1.5 KB)
 			const uint64_t floor_mbs = 1u << 15;         // one 4K frame and change
-			if (cap < chunk_mbs) chunk_mbs = cap > floor_mbs ? cap : floor_mbs;
+			if (cap < chunk_mbs_tok) chunk_mbs_tok = cap > floor_mbs ? cap : floor_mbs;
+			if (cap < chunk_mbs_pk) chunk_mbs_pk = cap > floor_mbs ? cap : floor_mbs;
 		}
 	}
 	for (uint32_t i = 0; i < n; i++) memset(&outs[i], 0, sizeof(outs[i]));
@@ -231,31 +278,37 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 	Feed feed;
 	feed.files = files;
 	feed.n = n;
-	feed.tok = tok;
 	feed.fflags = (flags & VP8G_BATCH_MULTI_PARTITION) ? VP8F_MULTI_PARTITION : 0u;
+	feed.pk.assign(n, Vp8gPackedFrame{});
 	if (tok) feed.tj.assign(n, TokJob{});
-	else feed.pk.assign(n, Vp8gPackedFrame{});
 	feed.err.assign(n, 0);
 	feed.ready.reset(new uint8_t[n]());
+	plan_frames(files, n, tok, threads, feed.dev, feed.order);
+	const uint32_t chunk_frames = tok ? chunk_frames_tok : chunk_frames_pk;
 	const uint32_t window = 2 * chunk_frames > 4 * threads ? 2 * chunk_frames : 4 * threads;
 	feed.limit = window;
 	std::vector<std::thread> pool;
 	pool.reserve(threads);
 	for (uint32_t t = 0; t < threads; t++) pool.emplace_back([&feed] { feed.work(); });
 
-	hipStream_t stream = nullptr;  // uploads and kernels
-	hipStream_t copy = nullptr;    // downloads: chunk k's D2H overlaps chunk k+1's kernels
-	Slot slots[2];
-	uint32_t released = 0;  // frames whose packed data is freed (all below this index)
+	// uploads and kernels on one stream per chunk slot (a long device-m05 chunk and the next
+	// chunk's kernels overlap); downloads on `copy`: chunk k's D2H overlaps chunk k+1's kernels
+	// slots 0/1 alternate between device-m05 chunks, 2/3 between host-m05 chunks, so a hybrid batch's
+	// host chunks never wait for the (long) device-m05 chunk's slot
+	hipStream_t streams[4] = {nullptr, nullptr, nullptr, nullptr};
+	hipStream_t copy = nullptr;
+	Slot slots[4];
+	uint32_t nchunk[2] = {0, 0};  // chunks so far per kind (host, device)
+	uint32_t released = 0;  // positions whose frames' host data is freed (all below this one)
 	const char* where = nullptr;
 	hipError_t he = hipSuccess;
 	auto release = [&](Slot& s) {
-		if (!tok)
-			for (uint32_t i : s.frames) vp8f_packed_free(&feed.pk[i]);
+		for (uint32_t i : s.frames)
+			if (!feed.dev[i]) vp8f_packed_free(&feed.pk[i]);
 		s.frames.clear();
 	};
-	auto kf_of = [&](uint32_t i) -> const Vp8KeyFrameHeader& { return tok ? feed.tj[i].kf : feed.pk[i].kf; };
-	auto f_of = [&](uint32_t i) -> const Vp8DecodedFrame& { return tok ? feed.tj[i].hdr : feed.pk[i].f; };
+	auto kf_of = [&](uint32_t i) -> const Vp8KeyFrameHeader& { return feed.dev[i] ? feed.tj[i].kf : feed.pk[i].kf; };
+	auto f_of = [&](uint32_t i) -> const Vp8DecodedFrame& { return feed.dev[i] ? feed.tj[i].hdr : feed.pk[i].f; };
 	auto finish_slot = [&](Slot& s) -> bool {  // wait for a slot's chunk; false on a device failure
 		if (!s.busy) return true;
 		s.busy = false;
@@ -280,7 +333,7 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 		}                            \
 	} while (0)
 
-	PTRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "stream");
+	for (hipStream_t& st : streams) PTRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "stream");
 	PTRY(hipStreamCreateWithFlags(&copy, hipStreamNonBlocking), "stream");
 	for (Slot& s : slots) {
 		PTRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), "event");
@@ -288,28 +341,35 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 	}
 
 	{
-		uint32_t a = 0, chunk = 0;
+		uint32_t a = 0;
 		while (a < n) {
-			// -- gather the next chunk: consecutive frames, in order, as they finish
+			// -- gather the next chunk: consecutive positions of one kind (device m05 or host m05),
+			// in order, as they finish
 			std::vector<uint32_t> idx;
 			uint64_t mbs = 0, vals = 0, bitsb = 0, outb = 0;
 			uint32_t b = a, max_cols = 0, max_rows = 0;
-			while (b < n && b - a < chunk_frames) {
-				feed.wait_ready(b);
-				if (feed.err[b] == 0) {
-					const Vp8DecodedFrame& f = f_of(b);
-					if (!idx.empty() && mbs + f.mb_total > chunk_mbs) break;
-					idx.push_back(b);
+			const bool ctok = feed.dev[feed.order[a]] != 0;  // this chunk's kind
+			const uint32_t cframes = ctok ? chunk_frames_tok : chunk_frames_pk;
+			const uint64_t cmbs = ctok ? chunk_mbs_tok : chunk_mbs_pk;
+			while (b < n && b - a < cframes && (feed.dev[feed.order[b]] != 0) == ctok) {
+				const uint32_t fi = feed.order[b];
+				feed.wait_ready(fi);
+				if (feed.err[fi] == 0) {
+					const Vp8DecodedFrame& f = f_of(fi);
+					if (!idx.empty() && mbs + f.mb_total > cmbs) break;
+					idx.push_back(fi);
 					mbs += f.mb_total;
-					if (tok) bitsb += bits_slot(feed.tj[b].psize);
-					else vals += feed.pk[b].n_values;
-					outb = al256(outb + vp8g_i420_size(kf_of(b).width, kf_of(b).height));
+					if (ctok) bitsb += bits_slot(feed.tj[fi].psize);
+					else vals += feed.pk[fi].n_values;
+					outb = al256(outb + vp8g_i420_size(kf_of(fi).width, kf_of(fi).height));
 					if (f.mb_cols > max_cols) max_cols = f.mb_cols;
 					if (f.mb_rows > max_rows) max_rows = f.mb_rows;
 				}
 				b++;
 			}
-			Slot& s = slots[chunk & 1];
+			const uint32_t si = (ctok ? 0u : 2u) + (nchunk[ctok ? 1 : 0]++ & 1u);
+			Slot& s = slots[si];
+			hipStream_t stream = streams[si];
 			if (!finish_slot(s)) goto fail;
 			if (idx.empty()) {
 				a = b;
@@ -328,15 +388,15 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 			L.seg = o, o = al256(o + mbs);
 			L.hasc = o, o = al256(o + mbs);
 			L.bm = o, o = al256(o + mbs * 16);
-			L.masks = o, o = al256(o + (tok ? 0 : mbs * kNb * 2));
-			L.mboff = o, o = al256(o + (tok ? 0 : mbs * 4));
-			L.vals = o, o = al256(o + (tok ? 0 : vals * 2 + 64));  // +64: the expansion may address one past the end
+			L.masks = o, o = al256(o + (ctok ? 0 : mbs * kNb * 2));
+			L.mboff = o, o = al256(o + (ctok ? 0 : mbs * 4));
+			L.vals = o, o = al256(o + (ctok ? 0 : vals * 2 + 64));  // +64: the expansion may address one past the end
 			L.cy = o, o = al256(o + mbs * 512);
 			L.cu = o, o = al256(o + mbs * 128);
 			L.cv = o, o = al256(o + mbs * 128);
 			L.cy2 = o, o = al256(o + mbs * 32);
 			L.bits = o, o = al256(o + bitsb);
-			L.jobs = o, o = al256(o + (tok ? nf * sizeof(Vp8gTokFrame) : 0));
+			L.jobs = o, o = al256(o + (ctok ? nf * sizeof(Vp8gTokFrame) : 0));
 			L.desc = o, o = al256(o + nf * sizeof(Vp8gFrameDesc));
 			L.status = o, o = al256(o + 4);
 			L.gctx = o, o = al256(o + (big ? (uint64_t)nf * max_cols * vp8g::kCtxBytesPerCol : 0));
@@ -348,7 +408,7 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 			uint8_t* d = s.buf;
 			// -- descriptors and output images
 			s.descs.assign(nf, Vp8gFrameDesc{});
-			if (tok) {
+			if (ctok) {
 				s.jobs.resize(nf);
 				uint64_t mo = 0, bo = 0, oo = 0;
 				for (uint32_t j = 0; j < nf; j++) {
@@ -413,7 +473,7 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 				arr.bmode = d + L.bm;
 				arr.src = nullptr;
 				arr.status = (uint32_t*)(d + L.status);
-				if (tok) {
+				if (ctok) {
 					PTRY(hipMemsetAsync(d + L.cy, 0, L.cy2 + mbs * 32 - L.cy, stream), "memset");
 					if (vp8g_m05_batch_device(s.jobs.data(), (const Vp8gTokFrame*)(d + L.jobs), nf, d + L.bits, &arr, stream) != 0) {
 						he = hipGetLastError();
@@ -452,7 +512,6 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 			released = b;
 			feed.set_limit(released + window);
 			a = b;
-			chunk++;
 		}
 		for (Slot& s : slots)
 			if (!finish_slot(s)) goto fail;
@@ -464,12 +523,12 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 		if (s.kdone) (void)hipEventDestroy(s.kdone);
 		if (s.buf) (void)hipFree(s.buf);
 	}
-	(void)hipStreamDestroy(stream);
+	for (hipStream_t st : streams) (void)hipStreamDestroy(st);
 	(void)hipStreamDestroy(copy);
 	{
 		int first = 0;
 		for (uint32_t i = 0; i < n; i++) {
-			if (!tok) vp8f_packed_free(&feed.pk[i]);  // failed frames (the others were freed per chunk)
+			if (!feed.dev[i]) vp8f_packed_free(&feed.pk[i]);  // failed frames (the others were freed per chunk)
 			if (status) status[i] = feed.err[i];
 			if (feed.err[i] && !first) first = feed.err[i];
 			if (feed.err[i]) yuv420_free(&outs[i]);
@@ -484,7 +543,8 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 fail:
 	feed.stop();
 	for (auto& t : pool) t.join();
-	if (stream) (void)hipStreamSynchronize(stream);
+	for (hipStream_t st : streams)
+		if (st) (void)hipStreamSynchronize(st);
 	if (copy) (void)hipStreamSynchronize(copy);
 	vp8g::set_error_text(where ? where : "pipeline", he);
 	for (Slot& s : slots) {
@@ -492,10 +552,11 @@ fail:
 		if (s.kdone) (void)hipEventDestroy(s.kdone);
 		if (s.buf) (void)hipFree(s.buf);
 	}
-	if (stream) (void)hipStreamDestroy(stream);
+	for (hipStream_t st : streams)
+		if (st) (void)hipStreamDestroy(st);
 	if (copy) (void)hipStreamDestroy(copy);
 	for (uint32_t i = 0; i < n; i++) {
-		if (!tok) vp8f_packed_free(&feed.pk[i]);
+		if (!feed.dev[i]) vp8f_packed_free(&feed.pk[i]);
 		yuv420_free(&outs[i]);
 		if (status) status[i] = EIO;
 	}
