@@ -15,9 +15,12 @@ for n in (256, 1024):
     res = {"frames": n}
     vp8g.gpu_decode_webp_batch(batch, True, thr)
     res["host_m05_s"] = round(vp8g.gpu_decode_webp_batch.seconds, 3)
-    for hn in ("10", "20", "30", "40", "50"):
+    for hn in (sys.argv[1:] or ["10", "20", "30", "40", "50"]):
         if hn == "off":
             os.environ["VP8G_HYBRID"] = "0"
+        elif hn == "default":  # the library's own constants
+            os.environ["VP8G_HYBRID"] = "1"
+            os.environ.pop("VP8G_HOST_NS_PER_BYTE", None)
         else:
             os.environ["VP8G_HYBRID"] = "1"
             os.environ["VP8G_HOST_NS_PER_BYTE"] = hn

@@ -19,10 +19,14 @@
 // m05 keeps global state (vp8_tokens.c:382, :625), which is why it cannot be threaded as is.
 #include <errno.h>
 #include <sched.h>
+#include <sys/mman.h>
+#include <unistd.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <atomic>
 #include <condition_variable>
 #include <memory>
@@ -174,6 +178,11 @@ struct Feed {
 };
 
 // One chunk's device buffer and the host state that must live until its copies are done.
+struct D2H {
+	void* dst;
+	const void* src;
+	size_t bytes;
+};
 struct Slot {
 	uint8_t* buf = nullptr;
 	size_t cap = 0;
@@ -184,6 +193,78 @@ struct Slot {
 	std::vector<Vp8gFrameDesc> descs;
 	std::vector<Vp8gTokFrame> jobs;  // device m05
 	uint32_t status = 0;
+	std::vector<D2H> d2h;          // the chunk's downloads (issued by a Copier)
+	bool issued = false;           // the Copier has issued them and recorded `done` (guarded by its mutex)
+	hipError_t copy_err = hipSuccess;
+};
+
+// Downloads into the callers' images are pageable-memory copies, which HIP completes
+// synchronously in the calling thread -- after waiting for the chunk's kernels.  Issued from
+// the thread that launches chunks, one long device-m05 chunk's download would hold up every
+// later launch (host-m05 chunks that are ready, the next device chunk).  Each Copier owns a
+// thread and a stream and issues the downloads of the chunks queued to it, in order.
+struct Copier {
+	std::thread th;
+	std::mutex mu;
+	std::condition_variable cv;
+	std::vector<Slot*> q;
+	size_t head = 0;
+	bool quit = false;
+	hipStream_t stream = nullptr;
+
+	void run() {
+		for (;;) {
+			Slot* s;
+			{
+				std::unique_lock<std::mutex> lk(mu);
+				cv.wait(lk, [&] { return head < q.size() || quit; });
+				if (quit) return;
+				s = q[head++];
+			}
+			// fresh output images fault their pages in during the copy, one 4-KB page at a time in
+			// this thread; populate them first, while the chunk's kernels still run
+			for (const D2H& c : s->d2h) prefault(c.dst, c.bytes);
+			hipError_t e = hipStreamWaitEvent(stream, s->kdone, 0);
+			for (const D2H& c : s->d2h)
+				if (e == hipSuccess) e = hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyDeviceToHost, stream);
+			if (e == hipSuccess) e = hipEventRecord(s->done, stream);
+			{
+				std::lock_guard<std::mutex> lk(mu);
+				s->issued = true;
+				s->copy_err = e;
+			}
+			cv.notify_all();
+		}
+	}
+	static void prefault(void* p, size_t bytes) {
+#ifndef MADV_POPULATE_WRITE
+#define MADV_POPULATE_WRITE 23
+#endif
+		static const uintptr_t pg = (uintptr_t)sysconf(_SC_PAGESIZE);
+		const uintptr_t a = ((uintptr_t)p + pg - 1) & ~(pg - 1), e = ((uintptr_t)p + bytes) & ~(pg - 1);
+		if (e > a) (void)madvise((void*)a, e - a, MADV_POPULATE_WRITE);  // (best effort: older kernels say EINVAL)
+	}
+	void push(Slot* s) {
+		{
+			std::lock_guard<std::mutex> lk(mu);
+			s->issued = false;
+			q.push_back(s);
+		}
+		cv.notify_all();
+	}
+	hipError_t wait_issued(Slot* s) {
+		std::unique_lock<std::mutex> lk(mu);
+		cv.wait(lk, [&] { return s->issued; });
+		return s->copy_err;
+	}
+	void stop() {
+		{
+			std::lock_guard<std::mutex> lk(mu);
+			quit = true;
+		}
+		cv.notify_all();
+		if (th.joinable()) th.join();
+	}
 };
 
 struct ChunkLayout {
@@ -204,15 +285,16 @@ hipError_t grow(Slot& s, size_t need) {
 
 // Which frames run m05 on the device and in which order the workers take them.  Without
 // VP8G_BATCH_DEVICE_M05 every frame is decoded on the host, in index order.  With it the device
-// runs m05 as one workgroup per frame, so a chunk lasts as long as its heaviest frame (per-frame
-// latency ~ kDevNsPerByte x payload bytes), while the host threads would otherwise only parse
-// headers: the heaviest frames go to the host threads (~ kHostNsPerByte x bytes each, `threads`
-// at a time) for as long as that keeps the host's share shorter than the device's
-// (VP8G_HYBRID=0 turns this off).  Device frames come first, so their chunks
-// launch while the host threads decode the heavy ones.
-constexpr double kDevNsPerByte = 850.0;   // device m05 latency, 4K fixtures
-constexpr double kHostNsPerByte = 35.0;   // host m05 into the packed format, one thread: effective value
-                                          // calibrated on the box (tools/hybrid_sweep.py, profiles/r02_hybrid.json)
+// runs m05 as one workgroup per frame, so the device part lasts as long as its heaviest frame
+// (latency ~ kDevNsPerByte x payload bytes) plus the download of all its images, while the host
+// threads would otherwise only parse headers.  So the heaviest frames go to the host threads
+// (~ kHostNsPerByte x bytes each, `threads` at a time): the k heaviest, for the k that minimises
+// max(host time, device time) (VP8G_HYBRID=0 turns this off).  Device frames come
+// first, so their chunk launches while the host threads decode the heavy ones.
+constexpr double kDevNsPerByte = 850.0;    // device m05 latency per payload byte, 4K fixtures
+constexpr double kHostNsPerByte = 50.0;    // host m05 into the packed format, per payload byte and thread
+constexpr double kD2HNsPerByte = 0.085;    // download into fresh pageable images (~12 GB/s)
+// (rates measured on the box: tools/e2e_probe.py chunk traces, tools/hybrid_sweep.py; profiles/r02_hybrid.json)
 void plan_frames(const ByteSpan* files, uint32_t n, bool tok, uint32_t threads, std::vector<uint8_t>& dev,
                  std::vector<uint32_t>& order) {
 	dev.assign(n, tok ? 1 : 0);
@@ -220,22 +302,34 @@ void plan_frames(const ByteSpan* files, uint32_t n, bool tok, uint32_t threads, 
 	for (uint32_t i = 0; i < n; i++) order[i] = i;
 	const char* hv = getenv("VP8G_HYBRID");
 	if (!tok || (hv && atoi(hv) == 0)) return;
-	double dev_per_b = kDevNsPerByte, host_per_b = kHostNsPerByte;
-	if (const char* e = getenv("VP8G_DEV_NS_PER_BYTE")) dev_per_b = atof(e);    // calibration knobs
+	double dev_per_b = kDevNsPerByte, host_per_b = kHostNsPerByte, d2h_per_b = kD2HNsPerByte;
+	if (const char* e = getenv("VP8G_DEV_NS_PER_BYTE")) dev_per_b = atof(e);  // calibration knobs
 	if (const char* e = getenv("VP8G_HOST_NS_PER_BYTE")) host_per_b = atof(e);
-	std::vector<uint32_t> by_size(order);
-	std::stable_sort(by_size.begin(), by_size.end(),
-	                 [&](uint32_t x, uint32_t y) { return files[x].size > files[y].size; });
-	double host_ns = 0;
-	const double thr = threads ? (double)threads : 1.0;
-	for (uint32_t k = 0; k < n; k++) {
-		const uint32_t f = by_size[k];
-		const double dev_ns = dev_per_b * (double)files[f].size;  // the heaviest frame still on the device
-		const double h = host_ns + host_per_b * (double)files[f].size / thr;
-		if (h > dev_ns) break;
-		host_ns = h;
-		dev[f] = 0;
+	if (const char* e = getenv("VP8G_D2H_NS_PER_BYTE")) d2h_per_b = atof(e);
+	std::vector<double> outb(n, 0.0);  // I420 bytes (0 for a file whose header does not parse: it fails anyway)
+	for (uint32_t i = 0; i < n; i++) {
+		WebPContainer c;
+		Vp8KeyFrameHeader kf;
+		if (files[i].data && webp_parse_simple_lossy(files[i], &c) == 0 &&
+		    vp8_parse_keyframe_header(ByteSpan{files[i].data + c.vp8_chunk_offset, c.vp8_chunk_size}, &kf) == 0)
+			outb[i] = (double)vp8g_i420_size(kf.width, kf.height);
 	}
+	std::vector<uint32_t> by_size(order);
+	std::stable_sort(by_size.begin(), by_size.end(), [&](uint32_t x, uint32_t y) { return files[x].size > files[y].size; });
+	double dev_out = 0;
+	for (uint32_t i = 0; i < n; i++) dev_out += outb[i];
+	const double thr = threads ? (double)threads : 1.0;
+	double host_ns = 0, best = dev_per_b * (double)files[by_size[0]].size + d2h_per_b * dev_out;
+	uint32_t best_k = 0;
+	for (uint32_t k = 1; k <= n; k++) {  // the k heaviest on the host
+		const uint32_t f = by_size[k - 1];
+		host_ns += host_per_b * (double)files[f].size / thr;
+		dev_out -= outb[f];
+		const double dev_ns = (k < n ? dev_per_b * (double)files[by_size[k]].size : 0.0) + d2h_per_b * dev_out;
+		const double t = host_ns > dev_ns ? host_ns : dev_ns;
+		if (t < best) best = t, best_k = k;
+	}
+	for (uint32_t k = 0; k < best_k; k++) dev[by_size[k]] = 0;
 	uint32_t p = 0;
 	for (uint32_t i = 0; i < n; i++)
 		if (dev[i]) order[p++] = i;
@@ -284,6 +378,16 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 	feed.err.assign(n, 0);
 	feed.ready.reset(new uint8_t[n]());
 	plan_frames(files, n, tok, threads, feed.dev, feed.order);
+	// VP8G_PIPE_TRACE=1: one stderr line per chunk (kind, frames, MBs, launch / retire times; diagnostics)
+	const bool trace = getenv("VP8G_PIPE_TRACE") && atoi(getenv("VP8G_PIPE_TRACE")) != 0;
+	const auto t_start = std::chrono::steady_clock::now();
+	auto ms_now = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count(); };
+	if (trace) {
+		uint32_t nd = 0;
+		for (uint32_t i = 0; i < n; i++) nd += feed.dev[i];
+		fprintf(stderr, "[pipe] n=%u threads=%u device_frames=%u host_frames=%u chunk_mbs_tok=%llu chunk_mbs_pk=%llu\n", n,
+		        threads, nd, n - nd, (unsigned long long)chunk_mbs_tok, (unsigned long long)chunk_mbs_pk);
+	}
 	const uint32_t chunk_frames = tok ? chunk_frames_tok : chunk_frames_pk;
 	const uint32_t window = 2 * chunk_frames > 4 * threads ? 2 * chunk_frames : 4 * threads;
 	feed.limit = window;
@@ -292,11 +396,11 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 	for (uint32_t t = 0; t < threads; t++) pool.emplace_back([&feed] { feed.work(); });
 
 	// uploads and kernels on one stream per chunk slot (a long device-m05 chunk and the next
-	// chunk's kernels overlap); downloads on `copy`: chunk k's D2H overlaps chunk k+1's kernels
+	// chunk's kernels overlap); downloads by the Copiers: chunk k's D2H overlaps chunk k+1's kernels
 	// slots 0/1 alternate between device-m05 chunks, 2/3 between host-m05 chunks, so a hybrid batch's
 	// host chunks never wait for the (long) device-m05 chunk's slot
 	hipStream_t streams[4] = {nullptr, nullptr, nullptr, nullptr};
-	hipStream_t copy = nullptr;
+	Copier copiers[2];  // downloads of host-m05 chunks / device-m05 chunks
 	Slot slots[4];
 	uint32_t nchunk[2] = {0, 0};  // chunks so far per kind (host, device)
 	uint32_t released = 0;  // positions whose frames' host data is freed (all below this one)
@@ -312,10 +416,16 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 	auto finish_slot = [&](Slot& s) -> bool {  // wait for a slot's chunk; false on a device failure
 		if (!s.busy) return true;
 		s.busy = false;
+		const double tw = trace ? ms_now() : 0.0;
+		if ((he = copiers[&s - slots < 2 ? 1 : 0].wait_issued(&s)) != hipSuccess) {
+			where = "D2H";
+			return false;
+		}
 		if ((he = hipEventSynchronize(s.done)) != hipSuccess) {
 			where = "sync";
 			return false;
 		}
+		if (trace) fprintf(stderr, "[pipe] slot %d retired at %.1f ms (waited %.1f ms)\n", (int)(&s - slots), ms_now(), ms_now() - tw);
 		release(s);
 		if (s.status != 0) {
 			where = "kernel status";
@@ -334,7 +444,10 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 	} while (0)
 
 	for (hipStream_t& st : streams) PTRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "stream");
-	PTRY(hipStreamCreateWithFlags(&copy, hipStreamNonBlocking), "stream");
+	for (Copier& c : copiers) {
+		PTRY(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking), "stream");
+		c.th = std::thread([&c] { c.run(); });
+	}
 	for (Slot& s : slots) {
 		PTRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), "event");
 		PTRY(hipEventCreateWithFlags(&s.kdone, hipEventDisableTiming), "event");
@@ -456,6 +569,9 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 				}
 			}
 			s.frames = idx;
+			if (trace)
+				fprintf(stderr, "[pipe] chunk %s slot %u frames=%u mbs=%llu launched at %.1f ms\n", ctok ? "device-m05" : "host-m05", si,
+				        nf, (unsigned long long)mbs, ms_now());
 			PTRY(hipMemcpyAsync(d + L.desc, s.descs.data(), nf * sizeof(Vp8gFrameDesc), hipMemcpyHostToDevice, stream), "H2D");
 			PTRY(hipMemsetAsync(d + L.status, 0, 4, stream), "memset");
 			if (k > 1) PTRY(hipMemsetAsync(d + L.gprog, 0, (size_t)nf * k * 4, stream), "memset");
@@ -494,20 +610,20 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 				                         k > 1 ? (uint32_t*)(d + L.gprog) : nullptr),
 				     "recon launch");
 			}
-			// -- D2H into the callers' images, on the copy stream once the kernels are done
+			// -- D2H into the callers' images, by this kind's Copier once the kernels are done
 			PTRY(hipEventRecord(s.kdone, stream), "event");
-			PTRY(hipStreamWaitEvent(copy, s.kdone, 0), "event");
+			s.d2h.clear();
 			for (uint32_t j = 0; j < nf; j++) {
 				const Vp8gFrameDesc& fd = s.descs[j];
 				Yuv420Image& img = outs[idx[j]];
 				if (!img.y) continue;
 				const size_t ysz = (size_t)fd.stride_y * fd.height, uvsz = (size_t)fd.stride_uv * ((fd.height + 1) / 2);
-				PTRY(hipMemcpyAsync(img.y, d + L.out + fd.out_y, ysz, hipMemcpyDeviceToHost, copy), "D2H");
-				PTRY(hipMemcpyAsync(img.u, d + L.out + fd.out_u, uvsz, hipMemcpyDeviceToHost, copy), "D2H");
-				PTRY(hipMemcpyAsync(img.v, d + L.out + fd.out_v, uvsz, hipMemcpyDeviceToHost, copy), "D2H");
+				s.d2h.push_back({img.y, d + L.out + fd.out_y, ysz});
+				s.d2h.push_back({img.u, d + L.out + fd.out_u, uvsz});
+				s.d2h.push_back({img.v, d + L.out + fd.out_v, uvsz});
 			}
-			PTRY(hipMemcpyAsync(&s.status, d + L.status, 4, hipMemcpyDeviceToHost, copy), "D2H");
-			PTRY(hipEventRecord(s.done, copy), "event");
+			s.d2h.push_back({&s.status, d + L.status, 4});
+			copiers[ctok ? 1 : 0].push(&s);
 			s.busy = true;
 			released = b;
 			feed.set_limit(released + window);
@@ -516,15 +632,18 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 		for (Slot& s : slots)
 			if (!finish_slot(s)) goto fail;
 	}
+	if (trace) fprintf(stderr, "[pipe] all chunks retired at %.1f ms\n", ms_now());
 	for (auto& t : pool) t.join();
 	pool.clear();
+	for (Copier& c : copiers) c.stop();
 	for (Slot& s : slots) {
 		if (s.done) (void)hipEventDestroy(s.done);
 		if (s.kdone) (void)hipEventDestroy(s.kdone);
 		if (s.buf) (void)hipFree(s.buf);
 	}
 	for (hipStream_t st : streams) (void)hipStreamDestroy(st);
-	(void)hipStreamDestroy(copy);
+	for (Copier& c : copiers) (void)hipStreamDestroy(c.stream);
+	if (trace) fprintf(stderr, "[pipe] buffers freed at %.1f ms\n", ms_now());
 	{
 		int first = 0;
 		for (uint32_t i = 0; i < n; i++) {
@@ -543,9 +662,11 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 fail:
 	feed.stop();
 	for (auto& t : pool) t.join();
+	for (Copier& c : copiers) c.stop();
 	for (hipStream_t st : streams)
 		if (st) (void)hipStreamSynchronize(st);
-	if (copy) (void)hipStreamSynchronize(copy);
+	for (Copier& c : copiers)
+		if (c.stream) (void)hipStreamSynchronize(c.stream);
 	vp8g::set_error_text(where ? where : "pipeline", he);
 	for (Slot& s : slots) {
 		if (s.done) (void)hipEventDestroy(s.done);
@@ -554,7 +675,8 @@ fail:
 	}
 	for (hipStream_t st : streams)
 		if (st) (void)hipStreamDestroy(st);
-	if (copy) (void)hipStreamDestroy(copy);
+	for (Copier& c : copiers)
+		if (c.stream) (void)hipStreamDestroy(c.stream);
 	for (uint32_t i = 0; i < n; i++) {
 		if (!feed.dev[i]) vp8f_packed_free(&feed.pk[i]);
 		yuv420_free(&outs[i]);
