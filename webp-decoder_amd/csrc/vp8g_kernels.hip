@@ -65,6 +65,7 @@ constexpr int kPrioTab[11] = {VP8G_PRIO_TABLE, VP8G_PRIO_LF, VP8G_PRIO_WHT};
 #ifdef VP8G_STAMPS
 __device__ unsigned long long g_vp8g_stamps[16];
 __device__ unsigned long long g_vp8g_wave_times[64];  // frame 0: per wave {start, end} s_memrealtime
+__device__ unsigned long long g_vp8g_wave_info[512 * 16 * 2];  // blocks < 512: per wave {HW_ID | XCC_ID << 32, end - start}
 #define STAMP(i)                                          \
 	do {                                                  \
 		const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
@@ -554,6 +555,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 	uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 	uint64_t st_prev = __builtin_amdgcn_s_memtime();
 	if (f == 0 && lane0 == 0 && wave < 32) g_vp8g_wave_times[2 * wave] = __builtin_amdgcn_s_memrealtime();
+	const uint64_t st_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
 
 	// Loads for one lane of one step: coefficient blocks (ln 0..24), bmode (25), side bytes (26..29).
@@ -1179,6 +1181,13 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 	if (lane0 == 0)
 		for (int i = 0; i < 8; i++) atomicAdd(&g_vp8g_stamps[i], (unsigned long long)st_acc[i]);
 	if (f == 0 && lane0 == 0 && wave < 32) g_vp8g_wave_times[2 * wave + 1] = __builtin_amdgcn_s_memrealtime();
+	if (blockIdx.x < 512 && wave < 16 && lane0 == 0) {
+		uint32_t hw, xcc;
+		asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+		asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+		g_vp8g_wave_info[2 * (blockIdx.x * 16 + wave)] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+		g_vp8g_wave_info[2 * (blockIdx.x * 16 + wave) + 1] = __builtin_amdgcn_s_memrealtime() - st_t0;
+	}
 	if (f == 0 && lane0 == 0 && wave == 0) {
 		g_vp8g_stamps[8] = __builtin_amdgcn_s_memtime();
 		g_vp8g_stamps[9] = __builtin_amdgcn_s_memrealtime();
@@ -1205,6 +1214,9 @@ hipError_t launch_t(const Vp8gFrameDesc* d_descs, uint32_t n, const Vp8gBatchArr
 #ifdef VP8G_STAMPS
 extern "C" __attribute__((visibility("default"))) int vp8g_debug_wave_times(unsigned long long* out) {
 	return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vp8g_wave_times), sizeof(unsigned long long) * 64) == hipSuccess ? 0 : -1;
+}
+extern "C" __attribute__((visibility("default"))) int vp8g_debug_wave_info(unsigned long long* out) {
+	return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vp8g_wave_info), sizeof(unsigned long long) * 512 * 16 * 2) == hipSuccess ? 0 : -1;
 }
 extern "C" __attribute__((visibility("default"))) int vp8g_debug_stamps(unsigned long long* out, int reset) {
 	if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vp8g_stamps), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
