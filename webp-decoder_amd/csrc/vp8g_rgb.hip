@@ -54,14 +54,19 @@ constexpr uint32_t kBlkFile = kBlk + 5u;           // ... plus its header
 constexpr uint32_t kPngPrefix = 43u;               // signature 8, IHDR 25, IDAT len/type 8, zlib 2
 constexpr uint32_t kPngRaw0 = kPngPrefix + 5u;     // file offset of the first pixel-stream byte
 constexpr uint32_t kCrcStart = 37u;                // IDAT CRC covers the chunk type + data
-constexpr int kTreeLevels = 10;                    // log2(kThreads)
 static_assert(kSpan % kThreads == 0 && kPerThread % 16 == 0, "span layout");
 
-// Tables shared by every task (13 KB): CRC-32 slice-by-8 tables T0..T7, then for the in-span
-// tree the nibble tables of Z_{32 * 2^l}, l = 0..9: tab[2048 + 128 l + 16 j + v] = Z(v << 4j).
+// Tables shared by every task (48 KB): CRC-32 slice-by-8 tables T0..T7, then the nibble tables
+// (tab[base + 128 i + 16 j + v] = Z(v << 4j)) of the operators that move a thread's CRC to the end
+// of the span: per lane L, Z_{(63 - L) * 32} (to the end of its wave's 2 KB), per wave w,
+// Z_{(15 - w) * 2048} (to the end of the span).  The span CRC is then a plain XOR over lanes and
+// waves: one 8-lookup operator per thread instead of a 10-level tree of them.
 constexpr int kSlice = 8;
 constexpr int kNibBase = kSlice * 256;
-constexpr int kTabWords = kNibBase + kTreeLevels * 8 * 16;
+constexpr int kWaves = kThreads / 64;
+constexpr int kLaneOps = kNibBase;
+constexpr int kWaveOps = kLaneOps + 64 * 128;
+constexpr int kTabWords = kWaveOps + kWaves * 128;
 
 struct CrcLds {
 	uint32_t tab[kTabWords];
@@ -308,36 +313,35 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8, 8))
 #pragma unroll
 				for (uint32_t i = 0; i < kPerThread / 4u; i += 2) c = crc_dword2(L.tab, c, 0u, 0u);
 			}
-			// -- 3. span CRC: tree over the 1024 thread CRCs (32 bytes each): levels 0..5 inside the
-			// wave (lane shuffles), then one partial per wave through LDS and levels 6..9 in wave 0.
-			// crc(lo || hi) = Z_|hi|(crc(lo)) ^ crc(hi); the Adler partials just add.
+			// -- 3. span CRC = XOR over threads t of Z_{(1023 - t) * 32}(crc_t): each lane moves its CRC
+			// to the end of its wave's 2 KB and the wave XOR-reduces; wave 0 moves the 16 wave CRCs to
+			// the end of the span and XOR-reduces them.  The Adler partials are plain sums (< 2^27 over
+			// a span), reduced mod 65521 once at the end.
 			const uint32_t lane = tid & 63u, wv = tid >> 6, par = tcount & 1u;
+			c = nib_apply(L.tab + kLaneOps + lane * 128u, c);
 #pragma unroll
 			for (int l = 0; l < 6; l++) {
-				const uint32_t oc = __shfl_down(c, 1u << l, 64), o0 = __shfl_down(s0, 1u << l, 64), o1 = __shfl_down(s1, 1u << l, 64);
-				c = nib_apply(L.tab + kNibBase + l * 128, c) ^ oc;
-				s0 = mod_add(s0, o0);
-				s1 = mod_add(s1, o1);
+				c ^= __shfl_xor(c, 1 << l, 64);
+				s0 += __shfl_xor(s0, 1 << l, 64);
+				s1 += __shfl_xor(s1, 1 << l, 64);
 			}
 			if (lane == 0) L.red[par][0][wv] = c, L.red[par][1][wv] = s0, L.red[par][2][wv] = s1;
 			__syncthreads();
 			if (wv == 0) {
-				c = lane < 16u ? L.red[par][0][lane] : 0u;
+				c = lane < 16u ? nib_apply(L.tab + kWaveOps + lane * 128u, L.red[par][0][lane]) : 0u;
 				s0 = lane < 16u ? L.red[par][1][lane] : 0u;
 				s1 = lane < 16u ? L.red[par][2][lane] : 0u;
 #pragma unroll
-				for (int l = 6; l < kTreeLevels; l++) {
-					const uint32_t sh = 1u << (l - 6);
-					const uint32_t oc = __shfl_down(c, sh, 16), o0 = __shfl_down(s0, sh, 16), o1 = __shfl_down(s1, sh, 16);
-					c = nib_apply(L.tab + kNibBase + l * 128, c) ^ oc;
-					s0 = mod_add(s0, o0);
-					s1 = mod_add(s1, o1);
+				for (int l = 0; l < 4; l++) {
+					c ^= __shfl_xor(c, 1 << l, 16);
+					s0 += __shfl_xor(s0, 1 << l, 16);
+					s1 += __shfl_xor(s1, 1 << l, 16);
 				}
 				if (lane == 0) {
 					uint32_t* pp = part + 4u * g;
 					pp[0] = c;
-					pp[1] = s0;
-					pp[2] = s1;
+					pp[1] = s0 % kMod;
+					pp[2] = s1 % kMod;
 				}
 			}
 			tcount++;
@@ -531,7 +535,7 @@ PngOps png_ops(uint32_t G, uint32_t zend) {
 	return o;
 }
 
-// the 8 KB constant tables, per device, built once
+// the 48 KB constant tables, per device, built once
 std::mutex g_tab_mu;
 uint32_t* g_tab_dev[64];
 
@@ -550,10 +554,12 @@ hipError_t tables_dev(uint32_t** out) {
 		}
 		for (int s = 1; s < kSlice; s++)
 			for (uint32_t b = 0; b < 256; b++) t[256 * s + b] = (t[256 * (s - 1) + b] >> 8) ^ t[t[256 * (s - 1) + b] & 255u];
-		Op z = op_zeros(kPerThread);
-		for (int l = 0; l < kTreeLevels; l++, z = op_mul(z, z))
+		auto put = [&](int base, const Op& z) {
 			for (int j = 0; j < 8; j++)
-				for (uint32_t v = 0; v < 16; v++) t[kNibBase + l * 128 + j * 16 + v] = op_host_apply(z, v << (4 * j));
+				for (uint32_t v = 0; v < 16; v++) t[base + j * 16 + v] = op_host_apply(z, v << (4 * j));
+		};
+		for (int l = 0; l < 64; l++) put(kLaneOps + 128 * l, op_zeros((uint64_t)(63 - l) * kPerThread));
+		for (int w = 0; w < kWaves; w++) put(kWaveOps + 128 * w, op_zeros((uint64_t)(kWaves - 1 - w) * 64u * kPerThread));
 		uint32_t* p = nullptr;
 		e = hipMalloc((void**)&p, kTabWords * 4);
 		if (e != hipSuccess) return e;
