@@ -16,6 +16,7 @@
 
 #include <stddef.h>
 #include <stdint.h>
+#include <string.h>
 
 typedef struct Vp8Bool Vp8Bool;
 
@@ -42,6 +43,15 @@ struct Vp8Bool {
 };
 
 static inline void vp8b_fill(Vp8Bool* b) {
+	if (b->bits < 0 && b->end - b->next >= 8) {
+		/* 7 bytes at once (big-endian): bits -7..-1 -> 49..55, value stays below 2^64 */
+		uint64_t w;
+		memcpy(&w, b->next, 8);
+		b->value = (b->value << 56) | (__builtin_bswap64(w) >> 8);
+		b->bits += 56;
+		b->next += 7;
+		return;
+	}
 	while (b->bits <= 48) {
 		uint64_t byte = 0;
 		if (b->next < b->end) byte = *b->next++;

@@ -94,11 +94,8 @@ static void note_overread_slow(TokenCtx* t, uint32_t mb, uint32_t plane, uint32_
 	st->token_overread_coeff_i = pos;
 	st->token_overread_stage = stage;
 }
-/* first position at which the partition was over-read (reference diagnostics, `decoder -info`) */
-#define NOTE_OVERREAD(t, mb, plane, blk, pos, stage) \
-	do { \
-		if ((t)->tok.shifts >= (t)->ovr_shift) note_overread_slow(t, mb, plane, blk, pos, stage); \
-	} while (0)
+/* (first position at which the partition was over-read: the reference diagnostics, `decoder -info`;
+ * read_block checks the shift count against TokenCtx.ovr_shift) */
 
 /* DCT_CAT1..6 magnitude: base + extra bits (RFC 6386 13.2) */
 static inline int read_cat(Vp8Bool* b, int cat) {
@@ -116,25 +113,37 @@ static inline int read_cat(Vp8Bool* b, int cat) {
  * diagnostics (0=Y 1=Y2 2=U 3=V). */
 static uint32_t read_block(TokenCtx* t, int type, int first, int ctx, int16_t out[16], uint32_t mb, uint32_t plane_tag,
                            uint32_t blk) {
-	Vp8CoeffStats* st = t->st;
-	Vp8Bool* b = &t->tok;
+	/* The bool decoder state and the statistics live in locals for the block: through the context
+	 * pointers every statistics store could alias the decoder state, which would then be reloaded
+	 * and stored around every bool. */
+	Vp8Bool bs = t->tok;
+	Vp8Bool* b = &bs;
+	const uint64_t ovr = t->ovr_shift;
+	uint32_t eobs = 0, nz = 0, amax = 0;
 	uint8_t(*P)[3][11] = t->probs[type];
 	memset(out, 0, 16 * sizeof(int16_t));
 	uint32_t mask = 0;
 	int pos = first;
 	const uint8_t* p = P[k_band[pos]][ctx];
 	int skip_eob = 0;
+#define NOTE_OVR(stage)                                                               \
+	do {                                                                              \
+		if (bs.shifts >= ovr) {                                                       \
+			t->tok = bs;                                                              \
+			note_overread_slow(t, mb, plane_tag, blk, (uint32_t)pos, (uint32_t)(stage)); \
+		}                                                                             \
+	} while (0)
 	while (pos < 16) {
 		if (!skip_eob) {
 			const int more = vp8b_read(b, p[0]);
 			if (!more) {
-				NOTE_OVERREAD(t, mb, plane_tag, blk, (uint32_t)pos, 0);
-				st->coeff_eob_tokens++;
+				NOTE_OVR(0);
+				eobs++;
 				break;
 			}
 		}
 		if (!vp8b_read(b, p[1])) { /* DCT_0 */
-			NOTE_OVERREAD(t, mb, plane_tag, blk, (uint32_t)pos, 0);
+			NOTE_OVR(0);
 			if (++pos == 16) break;
 			p = P[k_band[pos]][0];
 			skip_eob = 1;
@@ -143,32 +152,38 @@ static uint32_t read_block(TokenCtx* t, int type, int first, int ctx, int16_t ou
 		int mag;
 		if (!vp8b_read(b, p[2])) {
 			mag = 1;
-			NOTE_OVERREAD(t, mb, plane_tag, blk, (uint32_t)pos, 0);
+			NOTE_OVR(0);
 		} else {
 			if (!vp8b_read(b, p[3])) {
 				if (!vp8b_read(b, p[4])) mag = 2;
 				else mag = 3 + vp8b_read(b, p[5]);
-				NOTE_OVERREAD(t, mb, plane_tag, blk, (uint32_t)pos, 0);
+				NOTE_OVR(0);
 			} else {
 				int cat;
 				if (!vp8b_read(b, p[6])) cat = vp8b_read(b, p[7]);
 				else if (!vp8b_read(b, p[8])) cat = 2 + vp8b_read(b, p[9]);
 				else cat = 4 + vp8b_read(b, p[10]);
-				NOTE_OVERREAD(t, mb, plane_tag, blk, (uint32_t)pos, 0);
+				NOTE_OVR(0);
 				mag = read_cat(b, cat);
-				NOTE_OVERREAD(t, mb, plane_tag, blk, (uint32_t)pos, 1);
+				NOTE_OVR(1);
 			}
 		}
 		const int neg = vp8b_read(b, 128);
-		NOTE_OVERREAD(t, mb, plane_tag, blk, (uint32_t)pos, 2);
+		NOTE_OVR(2);
 		out[k_scan[pos]] = (int16_t)(neg ? -mag : mag);
 		mask |= 1u << k_scan[pos];
-		st->coeff_nonzero_total++;
-		if ((uint32_t)mag > st->coeff_abs_max) st->coeff_abs_max = (uint32_t)mag;
+		nz++;
+		if ((uint32_t)mag > amax) amax = (uint32_t)mag;
 		if (++pos == 16) break;
 		p = P[k_band[pos]][mag == 1 ? 1 : 2];
 		skip_eob = 0;
 	}
+#undef NOTE_OVR
+	t->tok = bs;
+	Vp8CoeffStats* st = t->st;
+	st->coeff_eob_tokens += eobs;
+	st->coeff_nonzero_total += nz;
+	if (amax > st->coeff_abs_max) st->coeff_abs_max = amax;
 	return mask;
 }
 
