@@ -491,7 +491,7 @@ struct Pref {
 // workgroup of 12 or 16 waves per CU for batches smaller than the CU count (pick_waves).  Either
 // way at most 4 waves per SIMD, i.e. the full 128-VGPR budget.
 template <int NW>
-constexpr int min_waves_per_simd() { return NW == 10 ? 5 : (NW >= 8 ? 4 : (NW >= 2 ? (2 * NW) / 4 : 1)); }
+constexpr int min_waves_per_simd() { return NW == 10 ? 5 : (NW >= 6 ? 4 : (NW >= 2 ? (2 * NW) / 4 : 1)); }
 
 // Split mode (kS, small batches): a frame's MB row pairs are dealt over `nsplit` workgroups
 // ("parts") of NW waves each -- global wave g = part * NW + wave owns pairs g, g + nsplit*NW, ...
@@ -1241,6 +1241,8 @@ int device_cus() {
 uint32_t pick_waves(uint32_t waves_hint, uint32_t max_mb_rows, uint32_t n_frames) {
 #ifdef VP8G_NW10  // diagnostic: 10 waves per frame at 5 waves per SIMD (needs the global context)
 	static const uint32_t kSupported[] = {1, 2, 4, 8, 10, 12, 16};
+#elif defined(VP8G_NW67)  // experiment: 6 / 7 waves per frame (fewer idle waves in a frame's last round)
+	static const uint32_t kSupported[] = {1, 2, 4, 6, 7, 8, 12, 16};
 #else
 	static const uint32_t kSupported[] = {1, 2, 4, 8, 12, 16};
 #endif
@@ -1291,6 +1293,10 @@ hipError_t launch_frames(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const 
 		VP8G_CASE(12)
 #ifdef VP8G_NW10
 		VP8G_CASE(10)
+#endif
+#ifdef VP8G_NW67
+		VP8G_CASE(6)
+		VP8G_CASE(7)
 #endif
 		default:
 		VP8G_CASE(16)
