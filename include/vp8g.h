@@ -275,6 +275,14 @@ int vp8g_decode_webp_batch(const ByteSpan* files, uint32_t n, int filtered, uint
 int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int filtered, uint32_t threads, uint32_t flags,
                               Yuv420Image* outs, int* status);
 
+/* The schedule vp8g_decode_webp_batch_ex uses for `flags` (host code only, no device call; for
+ * tests and tools): dev[i] = 1 if frame i's m05 runs on the device, 0 on the host threads;
+ * order[] = the order the worker threads take the frames (device frames first).  In device-m05
+ * mode the k heaviest payloads go to the host threads, k minimising max(host time, device
+ * time) under the library's cost model (VP8G_HYBRID=0 in the environment keeps
+ * every frame on the device).  0, or -1 + EINVAL. */
+int vp8g_plan_batch(const ByteSpan* files, uint32_t n, uint32_t threads, uint32_t flags, uint8_t* dev, uint32_t* order);
+
 /* Device m05 over n frames on `hip_stream`: h_jobs / d_jobs host and device copies of the jobs
  * (data = payload offset in d_bits, 4-aligned, with >= 512 readable bytes after the payload;
  * mb_offset = first MB in the arrays).  Writes ymode, uv_mode, segment_id, has_coeff, bmode and

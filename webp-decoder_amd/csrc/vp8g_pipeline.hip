@@ -339,6 +339,22 @@ void plan_frames(const ByteSpan* files, uint32_t n, bool tok, uint32_t threads, 
 
 }  // namespace
 
+VP8G_API int vp8g_plan_batch(const ByteSpan* files, uint32_t n, uint32_t threads, uint32_t flags, uint8_t* dev,
+                             uint32_t* order) {
+	if (!files || !dev || !order || n == 0 || (flags & ~(VP8G_BATCH_DEVICE_M05 | VP8G_BATCH_MULTI_PARTITION))) {
+		errno = EINVAL;
+		return -1;
+	}
+	std::vector<uint8_t> d;
+	std::vector<uint32_t> o;
+	uint32_t thr = threads ? threads : default_threads();
+	if (thr > n) thr = n;  // (as vp8g_decode_webp_batch_ex)
+	plan_frames(files, n, (flags & VP8G_BATCH_DEVICE_M05) != 0, thr, d, o);
+	memcpy(dev, d.data(), n);
+	memcpy(order, o.data(), n * sizeof(uint32_t));
+	return 0;
+}
+
 VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int filtered, uint32_t threads, uint32_t flags,
                                        Yuv420Image* outs, int* status) {
 	if (!files || !outs || n == 0 || (flags & ~(VP8G_BATCH_DEVICE_M05 | VP8G_BATCH_MULTI_PARTITION))) {
