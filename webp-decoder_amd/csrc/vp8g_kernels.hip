@@ -53,6 +53,9 @@ constexpr int kPrioTab[11] = {VP8G_PRIO_TABLE, VP8G_PRIO_LF, VP8G_PRIO_WHT};
 #ifndef VP8G_ABLATE
 #define VP8G_ABLATE 0
 #endif
+#ifndef VP8G_LF_SELECT  // loop filter: masked filter input by select instead of a branch (sel0)
+#define VP8G_LF_SELECT 0
+#endif
 // Bound of one dependency wait in s_memrealtime ticks (100 MHz): 2 s.  Test builds shorten it and
 // make one wave never publish its progress (VP8G_TEST_STALL_WAVE) to check that a stalled producer
 // ends the launch promptly with VP8G_ERR_TIMEOUT (tests/test_gpu_batch.py).
@@ -326,6 +329,19 @@ DEV void edge_mask(const int* x, bool en, int lim, int I, int T, bool& m, bool& 
 	hev = hm > T;
 }
 
+// m ? v : 0 as one v_cndmask (opaque to the optimiser, which otherwise turns the select into an
+// exec-masked branch around the filter arithmetic: cheaper for frames whose edges mostly fail the
+// masks, dearer for the frames that filter most edges -- and those set the launch time)
+DEV int sel0(bool m, int v) {
+#if VP8G_LF_SELECT
+	int r;
+	asm volatile("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(r) : "v"(v), "s"(__builtin_amdgcn_ballot_w64(m)));
+	return r;
+#else
+	return m ? v : 0;
+#endif
+}
+
 // Masking: the filter input (the common-adjust value) is zeroed where the edge mask is off, which
 // makes every tap 0 ((0 + 4) >> 3 = (0 + 3) >> 3 = (0 + 63) >> 7 = 0), so one select per edge
 // replaces one per delta and the pixel updates sat8(pixel +- delta) run unconditionally.
@@ -333,7 +349,7 @@ DEV void lf_mb_edge(int* x, bool en, int lim, int I, int T) {  // normal, MB edg
 	bool m, hev;
 	edge_mask(x, en, lim, I, T, m, hev);
 	const int p2 = x[1], p1 = x[2], p0 = x[3], q0 = x[4], q1 = x[5], q2 = x[6];
-	const int w = sclamp(m ? sclamp(p1 - q1) + __mul24(q0 - p0, 3) : 0);
+	const int w = sclamp(sel0(m, sclamp(p1 - q1) + __mul24(q0 - p0, 3)));
 	const int f1 = sclamp(w + 4) >> 3, f2 = sclamp(w + 3) >> 3;
 	const int a27 = (27 * w + 63) >> 7, a18 = (18 * w + 63) >> 7, a9 = (9 * w + 63) >> 7;
 	const int d0p = hev ? f2 : a27, d0q = hev ? f1 : a27;
@@ -350,7 +366,7 @@ DEV void lf_sub_edge(int* x, bool en, int lim, int I, int T) {  // normal, sub-b
 	bool m, hev;
 	edge_mask(x, en, lim, I, T, m, hev);
 	const int p1 = x[2], p0 = x[3], q0 = x[4], q1 = x[5];
-	const int a = m ? __mul24(q0 - p0, 3) + (hev ? sclamp(p1 - q1) : 0) : 0;
+	const int a = sel0(m, __mul24(q0 - p0, 3) + (hev ? sclamp(p1 - q1) : 0));
 	const int f1 = fshift(a, 4), f2 = fshift(a, 3);
 	const int a2 = hev ? 0 : (f1 + 1) >> 1;
 	x[4] = sat8(q0 - f1);
