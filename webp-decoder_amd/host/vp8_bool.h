@@ -93,6 +93,42 @@ static inline int vp8b_read(Vp8Bool* b, uint32_t prob) {
 	return bit;
 }
 
+/* One bool used as data, not as control (category extra bits, the odd bit of a 3/4 or of a
+ * category index): the same update as vp8b_read with selects instead of a branch. */
+static inline int vp8b_read_bit(Vp8Bool* b, uint32_t prob) {
+	const uint32_t split = 1u + (((b->range - 1u) * prob) >> 8);
+	const uint64_t big = (uint64_t)split << b->bits;
+	const int bit = b->value >= big;
+	const uint64_t m = 0u - (uint64_t)bit;
+	b->value -= big & m;
+	const uint32_t range = ((b->range - split) & (uint32_t)m) | (split & ~(uint32_t)m);
+	const int sh = __builtin_clz(range) - 24;
+	b->range = range << sh;
+	b->bits -= sh;
+	b->shifts += (uint64_t)sh;
+	if (b->bits < 0) vp8b_fill(b);
+	VP8B_TRACE(b, prob, bit);
+	return bit;
+}
+
+/* v or -v by one bool at probability 1/2 (a coefficient's sign: as likely one way as the other, so
+ * it is applied arithmetically rather than branched on) */
+static inline int vp8b_apply_sign(Vp8Bool* b, int v) {
+	const uint32_t split = 1u + ((b->range - 1u) >> 1);
+	const uint64_t big = (uint64_t)split << b->bits;
+	const int neg = b->value >= big;
+	const uint64_t m = 0u - (uint64_t)neg;
+	b->value -= big & m;
+	const uint32_t range = ((b->range - split) & (uint32_t)m) | (split & ~(uint32_t)m);
+	const int sh = __builtin_clz(range) - 24;
+	b->range = range << sh;
+	b->bits -= sh;
+	b->shifts += (uint64_t)sh;
+	if (b->bits < 0) vp8b_fill(b);
+	VP8B_TRACE(b, 128, neg);
+	return (v ^ -neg) + neg;
+}
+
 static inline uint32_t vp8b_literal(Vp8Bool* b, int n) {
 	uint32_t v = 0;
 	while (n-- > 0) v = (v << 1) | (uint32_t)vp8b_read(b, 128);

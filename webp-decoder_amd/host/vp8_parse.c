@@ -101,7 +101,7 @@ static void note_overread_slow(TokenCtx* t, uint32_t mb, uint32_t plane, uint32_
 static inline int read_cat(Vp8Bool* b, int cat) {
 	const uint8_t* ep = k_cat_probs[cat];
 	int extra = 0;
-	for (; *ep; ep++) extra = (extra << 1) | vp8b_read(b, *ep);
+	for (; *ep; ep++) extra = (extra << 1) | vp8b_read_bit(b, *ep);
 	return k_cat_base[cat] + extra;
 }
 
@@ -156,21 +156,21 @@ static uint32_t read_block(TokenCtx* t, int type, int first, int ctx, int16_t ou
 		} else {
 			if (!vp8b_read(b, p[3])) {
 				if (!vp8b_read(b, p[4])) mag = 2;
-				else mag = 3 + vp8b_read(b, p[5]);
+				else mag = 3 + vp8b_read_bit(b, p[5]);
 				NOTE_OVR(0);
 			} else {
 				int cat;
-				if (!vp8b_read(b, p[6])) cat = vp8b_read(b, p[7]);
-				else if (!vp8b_read(b, p[8])) cat = 2 + vp8b_read(b, p[9]);
-				else cat = 4 + vp8b_read(b, p[10]);
+				if (!vp8b_read(b, p[6])) cat = vp8b_read_bit(b, p[7]);
+				else if (!vp8b_read(b, p[8])) cat = 2 + vp8b_read_bit(b, p[9]);
+				else cat = 4 + vp8b_read_bit(b, p[10]);
 				NOTE_OVR(0);
 				mag = read_cat(b, cat);
 				NOTE_OVR(1);
 			}
 		}
-		const int neg = vp8b_read(b, 128);
+		const int sv = vp8b_apply_sign(b, mag);
 		NOTE_OVR(2);
-		out[k_scan[pos]] = (int16_t)(neg ? -mag : mag);
+		out[k_scan[pos]] = (int16_t)sv;
 		mask |= 1u << k_scan[pos];
 		nz++;
 		if ((uint32_t)mag > amax) amax = (uint32_t)mag;
