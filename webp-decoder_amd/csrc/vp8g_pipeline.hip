@@ -41,7 +41,7 @@
 
 namespace {
 
-constexpr uint32_t kChunkFrames = 64;          // frames per device chunk (at most)
+constexpr uint32_t kChunkFrames = 32;          // frames per host-m05 chunk (at most; tools/chunk_sweep.py: 32 shortens the tail)
 constexpr uint64_t kChunkMbs = 2u << 20;       // macroblocks per chunk (at most, unless one frame is bigger)
 // device m05: one workgroup per frame and a chunk's m05 time is its slowest frame's, so a chunk
 // wants as many frames as the chip runs at once (~1500 at full scalar-unit load): 1024 4K frames,
