@@ -60,6 +60,7 @@ WORKLOADS = {
 }
 FIXTURES = UHD  # (back-compat name used by tools/)
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+E2E_REPS = 3  # end-to-end legs: median of this many calls (host page-cache and allocator state vary call to call)
 TRAFFIC_FILE = ROOT / "profiles" / "traffic_4k_batch.json"
 
 
@@ -403,19 +404,23 @@ def end_to_end_device(manifest, n_frames, filtered, threads):
     files = [(ROOT / "tests" / "fixtures" / r).read_bytes() for r in UHD]
     batch = [files[i % 4] for i in range(n_frames)]
     vp8g.gpu_decode_webp_batch(batch[:8], filtered, threads, device_m05=True)  # warm
-    outs, st = vp8g.gpu_decode_webp_batch(batch, filtered, threads, device_m05=True)
-    dt = vp8g.gpu_decode_webp_batch.seconds  # the C call: .webp bytes -> I420 images
     key = "yuvf_sha256" if filtered else "yuv_sha256"
-    ok = all(s == 0 for s in st) and all(hashlib.sha256(outs[i]).hexdigest() == manifest["files"][UHD[i % 4]][key]
-                                         for i in range(n_frames))
-    del outs
+    runs, ok = [], True
+    for rep in range(E2E_REPS):  # median of E2E_REPS calls; every call's output checked
+        outs, st = vp8g.gpu_decode_webp_batch(batch, filtered, threads, device_m05=True)
+        runs.append(vp8g.gpu_decode_webp_batch.seconds)  # the C call: .webp bytes -> I420 images
+        ok = ok and all(s == 0 for s in st) and all(
+            hashlib.sha256(outs[i]).hexdigest() == manifest["files"][UHD[i % 4]][key]
+            for i in range(0, n_frames, 1 if rep == 0 else 16))  # first call: every frame; repeats: 1 in 16
+        del outs
+    dt = statistics.median(runs)
     return {"stage": "end to end with m05 on the device: .webp bytes in host memory -> I420 in host memory "
                      "(container + frame header on host threads; payload upload, m05 (one workgroup per frame), "
                      "recon+LF on the device; D2H; the heaviest frames' m05 on the host threads instead when that "
                      "finishes sooner)",
             "value": round(n_frames * 3840 * 2160 / 1e6 / dt, 1), "unit": "MP/s", "frames": n_frames,
-            "threads": threads, "seconds": round(dt, 3),
-            "parity": f"bit-exact vs reference ({n_frames} frames sha256)" if ok else "MISMATCH"}
+            "threads": threads, "seconds": round(dt, 3), "seconds_runs": [round(x, 3) for x in runs],
+            "parity": f"bit-exact vs reference ({n_frames} frames sha256; repeats sampled 1 in 16)" if ok else "MISMATCH"}
 
 
 def end_to_end(manifest, n_frames, filtered, threads):
@@ -427,16 +432,22 @@ def end_to_end(manifest, n_frames, filtered, threads):
     files = [(ROOT / "tests" / "fixtures" / r).read_bytes() for r in UHD]
     batch = [files[i % 4] for i in range(n_frames)]
     vp8g.gpu_decode_webp_batch(batch[:8], filtered, threads)  # warm: device buffers, code objects
-    outs, st = vp8g.gpu_decode_webp_batch(batch, filtered, threads)
-    dt = vp8g.gpu_decode_webp_batch.seconds  # the C call: .webp bytes -> I420 images
     key = "yuvf_sha256" if filtered else "yuv_sha256"
-    ok = all(s == 0 for s in st) and all(hashlib.sha256(outs[i]).hexdigest() == manifest["files"][UHD[i % 4]][key]
-                                         for i in range(n_frames))
+    runs, ok = [], True
+    for rep in range(E2E_REPS):  # median of E2E_REPS calls; every call's output checked
+        outs, st = vp8g.gpu_decode_webp_batch(batch, filtered, threads)
+        runs.append(vp8g.gpu_decode_webp_batch.seconds)  # the C call: .webp bytes -> I420 images
+        ok = ok and all(s == 0 for s in st) and all(
+            hashlib.sha256(outs[i]).hexdigest() == manifest["files"][UHD[i % 4]][key]
+            for i in range(0, n_frames, 1 if rep == 0 else 16))  # first call: every frame; repeats: 1 in 16
+        del outs
+    dt = statistics.median(runs)
     mp = n_frames * 3840 * 2160 / 1e6
     obj = {"stage": "end to end: .webp bytes in host memory -> I420 in host memory (container, header, m05 on host "
                     "threads into the packed format; upload, expansion, recon+LF on the device; D2H)",
            "value": round(mp / dt, 1), "unit": "MP/s", "frames": n_frames, "threads": threads,
-           "seconds": round(dt, 3), "parity": f"bit-exact vs reference ({n_frames} frames sha256)" if ok else "MISMATCH",
+           "seconds": round(dt, 3), "seconds_runs": [round(x, 3) for x in runs],
+           "parity": f"bit-exact vs reference ({n_frames} frames sha256; repeats sampled 1 in 16)" if ok else "MISMATCH",
            "reference_cli": None}
     dec = ROOT / "oracle" / "_ref" / "decoder"
     if dec.exists():
