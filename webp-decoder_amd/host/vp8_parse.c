@@ -110,14 +110,15 @@ static inline int read_cat(Vp8Bool* b, int cat) {
  * The token tree (13.2) is walked as straight code: node 0 (p[0]) EOB?, node 2
  * (p[1]) ZERO?, node 4 (p[2]) ONE?, then TWO/THREE/FOUR (p[3..5]) or the categories (p[6..10]);
  * after a ZERO the next token starts at node 2 (no EOB).  `plane_tag` is only for the overread
- * diagnostics (0=Y 1=Y2 2=U 3=V). */
-static uint32_t read_block(TokenCtx* t, int type, int first, int ctx, int16_t out[16], uint32_t mb, uint32_t plane_tag,
-                           uint32_t blk) {
-	/* The bool decoder state and the statistics live in locals for the block: through the context
-	 * pointers every statistics store could alias the decoder state, which would then be reloaded
-	 * and stored around every bool. */
-	Vp8Bool bs = t->tok;
-	Vp8Bool* b = &bs;
+ * diagnostics (0=Y 1=Y2 2=U 3=V).
+ * The bool decoder state and the statistics live in locals: through the context pointers every
+ * statistics store could alias the decoder state, which would then be reloaded and stored around
+ * every bool.  `checks` (a constant at each call) adds the reference's overread bookkeeping after
+ * every token; read_block runs without it and repeats a block with it only in the one block where
+ * the partition's overread first begins. */
+static inline __attribute__((always_inline)) uint32_t read_block_impl(TokenCtx* t, Vp8Bool* b, int type, int first, int ctx,
+                                                                      int16_t out[16], uint32_t mb, uint32_t plane_tag,
+                                                                      uint32_t blk, const int checks) {
 	const uint64_t ovr = t->ovr_shift;
 	uint32_t eobs = 0, nz = 0, amax = 0;
 	uint8_t(*P)[3][11] = t->probs[type];
@@ -126,12 +127,12 @@ static uint32_t read_block(TokenCtx* t, int type, int first, int ctx, int16_t ou
 	int pos = first;
 	const uint8_t* p = P[k_band[pos]][ctx];
 	int skip_eob = 0;
-#define NOTE_OVR(stage)                                                               \
-	do {                                                                              \
-		if (bs.shifts >= ovr) {                                                       \
-			t->tok = bs;                                                              \
-			note_overread_slow(t, mb, plane_tag, blk, (uint32_t)pos, (uint32_t)(stage)); \
-		}                                                                             \
+#define NOTE_OVR(stage)                                                                   \
+	do {                                                                                  \
+		if (checks && b->shifts >= ovr) {                                                 \
+			t->tok = *b;                                                                  \
+			note_overread_slow(t, mb, plane_tag, blk, (uint32_t)pos, (uint32_t)(stage));    \
+		}                                                                                 \
 	} while (0)
 	while (pos < 16) {
 		if (!skip_eob) {
@@ -179,11 +180,27 @@ static uint32_t read_block(TokenCtx* t, int type, int first, int ctx, int16_t ou
 		skip_eob = 0;
 	}
 #undef NOTE_OVR
-	t->tok = bs;
 	Vp8CoeffStats* st = t->st;
 	st->coeff_eob_tokens += eobs;
 	st->coeff_nonzero_total += nz;
 	if (amax > st->coeff_abs_max) st->coeff_abs_max = amax;
+	return mask;
+}
+
+static uint32_t read_block(TokenCtx* t, int type, int first, int ctx, int16_t out[16], uint32_t mb, uint32_t plane_tag,
+                           uint32_t blk) {
+	const Vp8Bool b0 = t->tok;
+	Vp8Bool bs = b0;
+	Vp8CoeffStats* st = t->st;
+	const uint32_t eob0 = st->coeff_eob_tokens, nz0 = st->coeff_nonzero_total, max0 = st->coeff_abs_max;
+	uint32_t mask = read_block_impl(t, &bs, type, first, ctx, out, mb, plane_tag, blk, 0);
+	if (bs.shifts >= t->ovr_shift && st->token_overread_mb_index == 0xFFFFFFFFu) {
+		/* the partition's overread begins in this block: decode it again, noting where */
+		st->coeff_eob_tokens = eob0, st->coeff_nonzero_total = nz0, st->coeff_abs_max = max0;
+		bs = b0;
+		mask = read_block_impl(t, &bs, type, first, ctx, out, mb, plane_tag, blk, 1);
+	}
+	t->tok = bs;
 	return mask;
 }
 
