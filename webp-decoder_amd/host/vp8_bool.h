@@ -7,9 +7,10 @@
  * partition read as zero (same as reference bool_decoder.c:5-15).
  *
  * The reference loads 2 bytes at init and then one byte every time 8 normalisation shifts
- * have accumulated (bool_decoder.c:17-39, :59-68).  We keep the total shift count `shifts`
- * so its diagnostic counters (bytes used / overread bytes, reported by `decoder -info`) can
- * be reproduced exactly without mimicking its byte-by-byte refill schedule.
+ * have accumulated (bool_decoder.c:17-39, :59-68).  The total shift count (vp8b_shifts) is what
+ * reproduces its diagnostic counters (bytes used / overread bytes, reported by `decoder -info`)
+ * without mimicking its byte-by-byte refill schedule.  It is not kept per bool: bits + shifts
+ * grows only by 8 per byte loaded, so shifts = 8 * (bytes loaded, padding included) - 8 - bits.
  */
 #ifndef VP8_BOOL_H
 #define VP8_BOOL_H
@@ -38,7 +39,8 @@ struct Vp8Bool {
 	uint64_t value;
 	int bits;        /* bits below the comparison window */
 	uint32_t range;  /* 128..255 between calls */
-	uint64_t shifts; /* total normalisation shifts so far */
+	const uint8_t* start; /* first byte of the partition */
+	uint64_t pad;         /* zero bytes shifted in past the end */
 	size_t size;     /* partition size in bytes */
 };
 
@@ -55,7 +57,7 @@ static inline void vp8b_fill(Vp8Bool* b) {
 	while (b->bits <= 48) {
 		uint64_t byte = 0;
 		if (b->next < b->end) byte = *b->next++;
-		/* past the end: shift in zeros (the coder's defined padding) */
+		else b->pad++; /* past the end: shift in zeros (the coder's defined padding) */
 		b->value = (b->value << 8) | byte;
 		b->bits += 8;
 	}
@@ -67,7 +69,8 @@ static inline void vp8b_init(Vp8Bool* b, const uint8_t* data, size_t size) {
 	b->value = 0;
 	b->bits = -8;
 	b->range = 255;
-	b->shifts = 0;
+	b->start = data;
+	b->pad = 0;
 	b->size = size;
 	vp8b_fill(b);
 }
@@ -87,7 +90,6 @@ static inline int vp8b_read(Vp8Bool* b, uint32_t prob) {
 	int sh = __builtin_clz(b->range) - 24;
 	b->range <<= sh;
 	b->bits -= sh;
-	b->shifts += (uint64_t)sh;
 	if (b->bits < 0) vp8b_fill(b);
 	VP8B_TRACE(b, prob, bit);
 	return bit;
@@ -105,7 +107,6 @@ static inline int vp8b_read_bit(Vp8Bool* b, uint32_t prob) {
 	const int sh = __builtin_clz(range) - 24;
 	b->range = range << sh;
 	b->bits -= sh;
-	b->shifts += (uint64_t)sh;
 	if (b->bits < 0) vp8b_fill(b);
 	VP8B_TRACE(b, prob, bit);
 	return bit;
@@ -123,7 +124,6 @@ static inline int vp8b_apply_sign(Vp8Bool* b, int v) {
 	const int sh = __builtin_clz(range) - 24;
 	b->range = range << sh;
 	b->bits -= sh;
-	b->shifts += (uint64_t)sh;
 	if (b->bits < 0) vp8b_fill(b);
 	VP8B_TRACE(b, 128, neg);
 	return (v ^ -neg) + neg;
@@ -152,7 +152,11 @@ static inline int vp8b_tree(Vp8Bool* b, const int8_t* tree, const uint8_t* probs
 }
 
 /* ---- reference-compatible diagnostics (see header comment) ---- */
-static inline uint64_t vp8b_ref_loads(const Vp8Bool* b) { return b->shifts >> 3; }
+/* total normalisation shifts so far (see the header comment) */
+static inline uint64_t vp8b_shifts(const Vp8Bool* b) {
+	return 8u * ((uint64_t)(b->next - b->start) + b->pad) - 8u - (uint64_t)(int64_t)b->bits;
+}
+static inline uint64_t vp8b_ref_loads(const Vp8Bool* b) { return vp8b_shifts(b) >> 3; }
 static inline size_t vp8b_ref_init_bytes(const Vp8Bool* b) { return b->size < 2 ? b->size : 2; }
 static inline uint32_t vp8b_ref_overread_bytes(const Vp8Bool* b) {
 	uint64_t avail = b->size - vp8b_ref_init_bytes(b);

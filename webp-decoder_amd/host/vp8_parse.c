@@ -129,7 +129,7 @@ static inline __attribute__((always_inline)) uint32_t read_block_impl(TokenCtx* 
 	int skip_eob = 0;
 #define NOTE_OVR(stage)                                                                   \
 	do {                                                                                  \
-		if (checks && b->shifts >= ovr) {                                                 \
+		if (checks && vp8b_shifts(b) >= ovr) {                                                 \
 			t->tok = *b;                                                                  \
 			note_overread_slow(t, mb, plane_tag, blk, (uint32_t)pos, (uint32_t)(stage));    \
 		}                                                                                 \
@@ -194,7 +194,7 @@ static uint32_t read_block(TokenCtx* t, int type, int first, int ctx, int16_t ou
 	Vp8CoeffStats* st = t->st;
 	const uint32_t eob0 = st->coeff_eob_tokens, nz0 = st->coeff_nonzero_total, max0 = st->coeff_abs_max;
 	uint32_t mask = read_block_impl(t, &bs, type, first, ctx, out, mb, plane_tag, blk, 0);
-	if (bs.shifts >= t->ovr_shift && st->token_overread_mb_index == 0xFFFFFFFFu) {
+	if (vp8b_shifts(&bs) >= t->ovr_shift && st->token_overread_mb_index == 0xFFFFFFFFu) {
 		/* the partition's overread begins in this block: decode it again, noting where */
 		st->coeff_eob_tokens = eob0, st->coeff_nonzero_total = nz0, st->coeff_abs_max = max0;
 		bs = b0;
