@@ -41,6 +41,27 @@ constexpr int kCtxBytesPerCol = kCtxRecBytes + kCtxLfBytes;
 
 constexpr int kMaxLds = 163840;
 
+// Launch order (cost-balanced placement).  A frame's time is set by its size and by how much its
+// loop filter filters (profiles/r02b_wave_placement.json: 4K frames at filter level 2 take 11.2 ms,
+// at 40-63 14.8 ms); workgroups b and b + CUs share a CU.  cost_class is a coarse log2 of
+// MBs x (64 + the frame's largest MB-edge limit 2E + I, halved for the simple filter): 4 classes
+// per octave, 0..127, higher = heavier.
+constexpr uint32_t kCostClasses = 128;
+__host__ __device__ inline uint32_t cost_class(const Vp8gFrameDesc& d) {
+	uint32_t s = 0;
+	if (d.flags & VP8G_F_LOOPFILTER) {
+		for (int g = 0; g < 4; g++)
+			for (int b = 0; b < 2; b++) {
+				const uint32_t v = 2u * d.lf[g][b][0] + d.lf[g][b][1];
+				s = v > s ? v : s;
+			}
+		if (d.flags & VP8G_F_SIMPLE) s >>= 1;
+	}
+	const uint64_t cost = (uint64_t)d.mb_cols * d.mb_rows * (64u + s);  // >= 64, < 2^30
+	const uint32_t lg = 63u - (uint32_t)__builtin_clzll(cost);
+	return 4u * lg + (uint32_t)((cost >> (lg - 2u)) & 3u);
+}
+
 inline size_t lds_bytes(int waves, uint32_t ctx_cols, bool global_ctx) {
 	return (size_t)kHdrBytes + (size_t)waves * kWaveBytes + (global_ctx ? 0 : (size_t)ctx_cols * kCtxBytesPerCol);
 }
@@ -53,7 +74,14 @@ inline size_t lds_bytes(int waves, uint32_t ctx_cols, bool global_ctx) {
 // `gprog` (n_frames * nsplit words, zeroed before the launch).
 hipError_t launch_frames(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const Vp8gBatchArrays& arrays,
                          uint8_t* d_out, uint32_t ctx_cols, uint32_t max_mb_rows, uint8_t* global_ctx,
-                         hipStream_t stream, uint32_t waves_hint, uint32_t nsplit, uint8_t* mbox, uint32_t* gprog);
+                         hipStream_t stream, uint32_t waves_hint, uint32_t nsplit, uint8_t* mbox, uint32_t* gprog,
+                         uint32_t ord_first = 0);
+// ord_first != 0 (unsplit launches of more than ord_first frames): workgroup w decodes the frame at
+// position p(w) of the batch sorted by descending cost_class (stable), where p(w) = w except for
+// the second ord_first workgroups, which take the next ord_first positions in reverse -- so the
+// heaviest frame shares its CU with the lightest of those -- ord_first = the CU count.  Returns
+// that value for a batch when it is worth it (classes differ, more frames than CUs), else 0.
+uint32_t pick_order(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint32_t nsplit);
 
 constexpr uint32_t kMaxSplit = 8;
 int device_cus();

@@ -53,6 +53,9 @@ constexpr int kPrioTab[11] = {VP8G_PRIO_TABLE, VP8G_PRIO_LF, VP8G_PRIO_WHT};
 #ifndef VP8G_ABLATE
 #define VP8G_ABLATE 0
 #endif
+#ifndef VP8G_LAUNDER  // step loop: invariant per-lane words and frame flags re-laundered every step
+#define VP8G_LAUNDER 1
+#endif
 #ifndef VP8G_LF_SELECT  // loop filter: masked filter input by select instead of a branch (sel0)
 #define VP8G_LF_SELECT 0
 #endif
@@ -519,22 +522,71 @@ constexpr int min_waves_per_simd() { return NW == 10 ? 5 : (NW >= 6 ? 4 : (NW >=
 // ahead of use (MI355X_MICROARCH.md, inter-workgroup visibility: sc1 payload + drained flag).
 // Requires every part of a frame to be resident at once: the host splits only batches of at most
 // one part per CU.
+// The frame workgroup blockIdx.x decodes under the cost-balanced launch order (pick_order in
+// vp8g_device.h): the position p of this workgroup in the sorted batch, then the frame at that
+// position -- a histogram of the n frames' cost classes gives p's class c and its rank r among
+// the frames of class c, and a block-wide ballot scan over the frames finds the r-th frame of
+// class c in index order (a stable sort, without sorting).  Runs before the workgroup's LDS is
+// initialised and uses its first bytes as scratch; ends with a barrier.
+template <int NT>
+DEV uint32_t ordered_frame(const Vp8gFrameDesc* descs, uint32_t n, uint32_t F, uint8_t* scratch) {
+	uint32_t* const hist = (uint32_t*)scratch;          // kCostClasses words
+	uint32_t* const wcnt = hist + kCostClasses;          // NT / 64 words
+	uint32_t* const found = wcnt + NT / 64;
+	const uint32_t tid = threadIdx.x, w = blockIdx.x;
+	const uint32_t S = min(n - F, F);
+	const uint32_t p = (w >= F && w < F + S) ? F + (F + S - 1u - w) : w;
+	for (uint32_t i = tid; i < kCostClasses; i += NT) hist[i] = 0u;
+	__syncthreads();
+	for (uint32_t i = tid; i < n; i += NT) atomicAdd(&hist[cost_class(descs[i])], 1u);
+	__syncthreads();
+	uint32_t acc = 0, cls = 0, r = 0;
+	for (int c = (int)kCostClasses - 1; c >= 0; c--) {  // descending cost
+		const uint32_t h = hist[c];
+		if (p >= acc && p < acc + h) cls = (uint32_t)c, r = p - acc;
+		acc += h;
+	}
+	const int wv = (int)(tid >> 6), lane = (int)(tid & 63);
+	uint32_t base = 0;  // frames of class cls before this chunk (block-uniform)
+	for (uint32_t c0 = 0; c0 < n; c0 += NT) {
+		const uint32_t i = c0 + tid;
+		const bool m = i < n && cost_class(descs[i]) == cls;
+		const uint64_t b = __ballot(m);
+		if (lane == 0) wcnt[wv] = (uint32_t)__popcll(b);
+		__syncthreads();
+		uint32_t off = base, tot = 0;
+		for (int q = 0; q < NT / 64; q++) {
+			const uint32_t cq = wcnt[q];
+			off += q < wv ? cq : 0u;
+			tot += cq;
+		}
+		if (m && off + (uint32_t)__popcll(b & ((1ull << lane) - 1ull)) == r) *found = i;
+		__syncthreads();
+		base += tot;
+		if (base > r) break;
+	}
+	const uint32_t f = (uint32_t)__builtin_amdgcn_readfirstlane((int)*found);
+	__syncthreads();
+	return f;
+}
+
 template <int NW, bool kG, bool kS>
 __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kernel(const Vp8gFrameDesc* __restrict__ descs, Vp8gBatchArrays A,
                                                         uint8_t* __restrict__ out, uint32_t ctx_cols,
                                                         uint8_t* __restrict__ gctx, uint32_t nsplit,
-                                                        uint8_t* __restrict__ mbox, uint32_t* __restrict__ gprog) {
+                                                        uint8_t* __restrict__ mbox, uint32_t* __restrict__ gprog,
+                                                        uint32_t ord_first) {
 	extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 	const int lane0 = (int)(threadIdx.x & 63);
 	const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
 	const uint32_t K = kS ? nsplit : 1u;
 	const uint32_t nfr = kS ? gridDim.x / K : gridDim.x;
-	const uint32_t f = kS ? blockIdx.x % nfr : blockIdx.x;
+	const uint32_t f = kS ? blockIdx.x % nfr : (ord_first ? ordered_frame<NW * 64>(descs, nfr, ord_first, smem) : blockIdx.x);
 	const uint32_t part = kS ? blockIdx.x / nfr : 0u;
 	const Vp8gFrameDesc& D = descs[f];
 
 	for (int i = (int)threadIdx.x; i < kBpModes * 64; i += NW * 64) ((uint32_t*)(smem + kBpTable))[i] = kBpTab.v[i];
-	const uint32_t bt_lane = kBorderTab.v[lane0 & 31];  // this lane's border-setup role (loop-invariant)
+	uint32_t bt_l = kBorderTab.v[lane0 & 31];  // this lane's border-setup role (loop-invariant)
 	if (threadIdx.x < 24) ((int16_t*)(smem + kDqTable))[threadIdx.x] = D.dq[threadIdx.x / 6][threadIdx.x % 6];
 	if (threadIdx.x < 32) smem[kLfTable + threadIdx.x] = D.lf[threadIdx.x >> 3][(threadIdx.x >> 2) & 1][threadIdx.x & 3];
 	if (threadIdx.x < 16) ((uint32_t*)(smem + kProgress))[threadIdx.x] = 0;
@@ -542,8 +594,9 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 
 	const uint32_t C = D.mb_cols, R = D.mb_rows;
 	const uint32_t flags = D.flags;
-	const bool lf_on = (flags & VP8G_F_LOOPFILTER) != 0;
-	const bool simple = (flags & VP8G_F_SIMPLE) != 0;
+	uint32_t flags_l = flags;  // (laundered per step, VP8G_LAUNDER)
+	[[maybe_unused]] const bool lf_on = (flags & VP8G_F_LOOPFILTER) != 0;
+	[[maybe_unused]] const bool simple = (flags & VP8G_F_SIMPLE) != 0;
 	const bool lf_only = (flags & VP8G_F_LF_ONLY) != 0;
 	const uint64_t mb0 = D.mb_offset;
 	uint8_t* const outY = out + D.out_y;
@@ -658,6 +711,15 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			// lane-dependent LDS addresses out of the loop would exhaust the VGPR budget.
 			int lane = lane0;
 			asm volatile("" : "+v"(lane));
+#if VP8G_LAUNDER
+			// The same for the loop-invariant per-lane words and the frame flags: comparisons on them
+			// would otherwise be hoisted as 64-bit lane masks, which exhaust the SGPRs and are spilled
+			// to VGPR lanes (a v_readlane pair, plus a hazard wait, per use per step).
+			asm volatile("" : "+v"(bt_l), "+v"(fl_bits), "+s"(flags_l));
+			const bool lf_on = (flags_l & VP8G_F_LOOPFILTER) != 0;
+			const bool simple = (flags_l & VP8G_F_SIMPLE) != 0;
+			const bool lf_only = (flags_l & VP8G_F_LF_ONLY) != 0;
+#endif
 			const int hh = lane >> 5, ln = lane & 31;
 			const uint32_t r = rA + (uint32_t)hh;
 			const int c = (int)t - 2 * hh;
@@ -850,7 +912,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					// the padded width's last byte, replicated), 5..8 chroma above rows -- 127 on the
 					// top row; 9..16 left columns at the frame's left edge (129); 17..19 the corners
 					// there (byte 3 of the word: 127 on the top row, else 129).
-					const uint32_t bt = bt_lane;
+					const uint32_t bt = bt_l;
 					const bool clampc = ln == 4 && cu + 1 == C;
 					const uint32_t rsrc = rec_off(cu + ((ln == 4 && !clampc) ? 1u : 0u)) + (clampc ? 12u : ((bt >> 12) & 0xFFu));
 					const uint32_t ldv = ctx.rd(rsrc);
@@ -1213,7 +1275,8 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 
 template <int NW, bool kG, bool kS>
 hipError_t launch_t(const Vp8gFrameDesc* d_descs, uint32_t n, const Vp8gBatchArrays& arrays, uint8_t* d_out,
-                    uint32_t ctx_cols, uint8_t* gctx, uint32_t nsplit, uint8_t* mbox, uint32_t* gprog, hipStream_t stream) {
+                    uint32_t ctx_cols, uint8_t* gctx, uint32_t nsplit, uint8_t* mbox, uint32_t* gprog, hipStream_t stream,
+                    uint32_t ord_first = 0) {
 	const size_t lds = lds_bytes(NW, ctx_cols, kG);
 	auto fn = frame_kernel<NW, kG, kS>;
 	if (lds > 65536) {
@@ -1221,7 +1284,7 @@ hipError_t launch_t(const Vp8gFrameDesc* d_descs, uint32_t n, const Vp8gBatchArr
 		if (e != hipSuccess) return e;
 	}
 	hipLaunchKernelGGL(fn, dim3(n * (kS ? nsplit : 1u)), dim3(NW * 64), lds, stream, d_descs, arrays, d_out, ctx_cols, gctx,
-	                   nsplit, mbox, gprog);
+	                   nsplit, mbox, gprog, kS ? 0u : ord_first);
 	return hipGetLastError();
 }
 
@@ -1286,10 +1349,28 @@ uint32_t pick_split(uint32_t split_hint, uint32_t n_frames, uint32_t nw, uint32_
 	return k ? k : 1;
 }
 
+uint32_t pick_order(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint32_t nsplit) {
+	static const bool off = [] {  // VP8G_ORDER=0: launch in batch order (A/B experiments)
+		const char* e = getenv("VP8G_ORDER");
+		return e && e[0] == '0';
+	}();
+#ifdef VP8G_NO_ORDER  // diagnostic build: batch order always
+	return 0;
+#endif
+	const int n_cus = device_cus();
+	if (off || nsplit > 1 || n_cus <= 0 || n_frames <= (uint32_t)n_cus) return 0;
+	const uint32_t c0 = cost_class(h_descs[0]);
+	for (uint32_t i = 1; i < n_frames; i++)
+		if (cost_class(h_descs[i]) != c0) return (uint32_t)n_cus;
+	return 0;  // uniform batch: the order would be the identity
+}
+
 hipError_t launch_frames(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const Vp8gBatchArrays& arrays,
                          uint8_t* d_out, uint32_t ctx_cols, uint32_t max_mb_rows, uint8_t* global_ctx,
-                         hipStream_t stream, uint32_t waves_hint, uint32_t nsplit, uint8_t* mbox, uint32_t* gprog) {
+                         hipStream_t stream, uint32_t waves_hint, uint32_t nsplit, uint8_t* mbox, uint32_t* gprog,
+                         uint32_t ord_first) {
 	if (n_frames == 0) return hipSuccess;
+	if (ord_first >= n_frames) ord_first = 0;  // (the order maps positions >= ord_first; needs n > ord_first)
 	const uint32_t nw = pick_waves(waves_hint, max_mb_rows, n_frames);
 	const bool g = global_ctx != nullptr;
 	if (nsplit > 1 && !g && (nw == 8 || nw == 16)) {
@@ -1299,8 +1380,9 @@ hipError_t launch_frames(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const 
 	}
 #define VP8G_CASE(N)                                                                                                          \
 	case N:                                                                                                                   \
-		return g ? launch_t<N, true, false>(d_descs, n_frames, arrays, d_out, ctx_cols, global_ctx, 1, nullptr, nullptr, stream) \
-		         : launch_t<N, false, false>(d_descs, n_frames, arrays, d_out, ctx_cols, nullptr, 1, nullptr, nullptr, stream);
+		return g ? launch_t<N, true, false>(d_descs, n_frames, arrays, d_out, ctx_cols, global_ctx, 1, nullptr, nullptr, stream, \
+		                                    ord_first)                                                                        \
+		         : launch_t<N, false, false>(d_descs, n_frames, arrays, d_out, ctx_cols, nullptr, 1, nullptr, nullptr, stream, ord_first);
 	switch (nw) {
 		VP8G_CASE(1)
 		VP8G_CASE(2)

@@ -220,7 +220,8 @@ int run_locked(const std::vector<Vp8gFrameDesc>& descs, const Vp8gBatchArrays& a
 		gprog = (uint32_t*)(g_dev.mbox + mb);
 		HIP_TRY(hipMemsetAsync(gprog, 0, pb, s), "memset(progress)");
 	}
-	HIP_TRY(vp8g::launch_frames((const Vp8gFrameDesc*)d_descs, n, arr, d_out, max_cols, max_rows, gctx, s, nw, k, mbox, gprog),
+	const uint32_t ord = vp8g::pick_order(descs.data(), n, k);  // cost-balanced placement (vp8g_device.h)
+	HIP_TRY(vp8g::launch_frames((const Vp8gFrameDesc*)d_descs, n, arr, d_out, max_cols, max_rows, gctx, s, nw, k, mbox, gprog, ord),
 	        "launch");
 	return 0;
 }
