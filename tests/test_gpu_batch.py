@@ -4,6 +4,7 @@ reference decoder's own I420 (tests/golden/digests.json).
 
 * 260 x 4K (> 256 CUs: the launcher picks the timed `frame_kernel<8, false, false>`, no split);
 * 1100 x 1080p (the fhd4 workload's geometry);
+* 300 mixed 4K / 1080p frames in a scrambled order (the cost-balanced launch order);
 * 64 distinct synthetic 4K frames of the bench's synthetic batch (seed 0x5EED ^ i);
 * the digest kernel against the numpy restatement on odd sizes (tail words, unaligned lengths);
 * a stalled producer (test build lib/diag/libvp8g_stall.so: one wave never publishes, waits give
@@ -69,6 +70,34 @@ def test_device_batch_260_uhd_every_slot(vp8g, digests, filtered):
 def test_device_batch_1100_fhd_every_slot(vp8g, digests):
     b, bad = run_batch(vp8g, FHD, 1100, True, digests)
     assert not bad, f"{len(bad)} of 1100 slots differ, e.g. {bad[:8]}"
+    del b
+    torch.cuda.empty_cache()
+
+
+def test_device_batch_mixed_sizes_launch_order(vp8g, digests):
+    """300 slots mixing 4K and 1080p frames of all eight filter setups in a scrambled order: more
+    frames than CUs and differing cost classes, so the kernel runs under the cost-balanced launch
+    order (workgroup -> frame by the in-kernel histogram + ballot scan, csrc/vp8g_device.h
+    cost_class); every slot must still hold its own frame's reference output."""
+    import vp8g_batch
+    rels = UHD + FHD
+    frames = [vp8g.decode_file(FIXTURES / r) for r in rels]
+    n = 300
+    rng = np.random.default_rng(7)
+    pick = rng.integers(0, len(rels), n)
+    b = vp8g_batch.DeviceBatch(n, 3840, 2160, torch.device("cuda:0"))
+    for i, j in enumerate(pick):
+        b.place(i, frames[j], True)
+    b.commit()
+    stream = torch.cuda.current_stream().cuda_stream
+    b.launch(stream)
+    got = b.digests(stream)
+    assert b.status_word() == 0
+    exp = [int(digests["fixtures"][rels[j]]["yuvf"], 16) for j in pick]
+    bad = [i for i in range(n) if int(got[i]) != exp[i]]
+    assert not bad, f"{len(bad)} of {n} slots differ, e.g. {bad[:8]}"
+    for f in frames:
+        f.free()
     del b
     torch.cuda.empty_cache()
 

@@ -81,6 +81,17 @@ class DeviceBatch:
             seg.copy_(torch.from_numpy(f.array(name)))
         self.h_descs[i] = vp8g.make_desc(f, filtered, i * self.mb_per, i * self.frame_bytes)
 
+    def place(self, i: int, f: vp8g.Frame, filtered: bool):
+        """Upload a frame no larger than the batch geometry into slot i (mixed-size batches: the
+        frame's MBs and I420 output start at the slot's base; its descriptor carries its own size)."""
+        if f.mb_total > self.mb_per or vp8g.i420_size(f.width, f.height) > self.frame_bytes:
+            raise ValueError(f"frame {f.width}x{f.height} does not fit a {self.width}x{self.height} slot")
+        for name in ARRAY_NAMES:
+            per = _PER[name][1]
+            o = i * self.mb_per * per
+            self.arrays[name][o:o + f.mb_total * per].copy_(torch.from_numpy(f.array(name)))
+        self.h_descs[i] = vp8g.make_desc(f, filtered, i * self.mb_per, i * self.frame_bytes)
+
     def commit(self):
         """Descriptors to the device (after every slot is filled)."""
         self.d_descs = torch.frombuffer(bytearray(bytes(self.h_descs)), dtype=torch.uint8).to(self.dev)
