@@ -77,10 +77,11 @@ hipError_t launch_frames(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const 
                          hipStream_t stream, uint32_t waves_hint, uint32_t nsplit, uint8_t* mbox, uint32_t* gprog,
                          uint32_t ord_first = 0);
 // ord_first != 0 (unsplit launches of more than ord_first frames): workgroup w decodes the frame at
-// position p(w) of the batch sorted by descending cost_class (stable), where p(w) = w except for
-// the second ord_first workgroups, which take the next ord_first positions in reverse -- so the
-// heaviest frame shares its CU with the lightest of those -- ord_first = the CU count.  Returns
-// that value for a batch when it is worth it (classes differ, more frames than CUs), else 0.
+// position p(w) of the batch sorted by descending cost_class (stable): the first F = ord_first
+// workgroups the F heaviest frames, the next S = min(n - F, F) the S lightest in reverse (so the
+// heaviest frame shares its CU with the lightest), the rest the middle positions heaviest first.
+// pick_order returns F = the CU count when that is worth it (classes differ, more frames than
+// CUs), else 0.
 uint32_t pick_order(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint32_t nsplit);
 
 constexpr uint32_t kMaxSplit = 8;

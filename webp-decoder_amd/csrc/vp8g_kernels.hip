@@ -535,7 +535,9 @@ DEV uint32_t ordered_frame(const Vp8gFrameDesc* descs, uint32_t n, uint32_t F, u
 	uint32_t* const found = wcnt + NT / 64;
 	const uint32_t tid = threadIdx.x, w = blockIdx.x;
 	const uint32_t S = min(n - F, F);
-	const uint32_t p = (w >= F && w < F + S) ? F + (F + S - 1u - w) : w;
+	// the first F workgroups take the F heaviest frames, the next S the S lightest (lightest first,
+	// so the heaviest frame shares its CU with the lightest), the rest the middle, heaviest first
+	const uint32_t p = w < F ? w : (w < F + S ? n - 1u - (w - F) : w - S);
 	for (uint32_t i = tid; i < kCostClasses; i += NT) hist[i] = 0u;
 	__syncthreads();
 	for (uint32_t i = tid; i < n; i += NT) atomicAdd(&hist[cost_class(descs[i])], 1u);
