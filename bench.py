@@ -19,6 +19,7 @@ Workloads (--workload; the headline is uhd4, the other two are reported beside i
   fhd4   2048 x 1920x1080 per GPU: the 4 1080p fixtures (tests/fixtures/big/fhd_*), same scheme.
   synth  512 x 3840x2160 per GPU, all distinct: vp8_synth.c profile 0 ("measured-like"), seed
          0x5EED ^ global frame index (SURVEY.md §8(d) second mode).
+  uhd4_yuv  the uhd4 batch with -yuv semantics (m06 reconstruction only, no loop filter).
 Parity: after timing, vp8g_frame_digests digests every slot's output on the device; every rank's
 digests are gathered and compared with tests/golden/digests.json (the digest of the reference
 decoder's own I420 for that input) -- every frame of every rank, no pixel copies.
@@ -30,8 +31,9 @@ launch measured by rocprofv3 (profiles/traffic_4k_batch.json).
 
 cpu_baseline (rank 0, N = 1 only): the reference's own m06+m07 (oracle/_ref/libref.so, compiled from
 the reference sources) when present, else our C restatement (oracle/liboracle.so), on a bounded
-sample of the same frames, one frame per thread, threads = this process's CPU share
-(OMP_NUM_THREADS if set -- 16 per GPU on the GPU box -- else the affinity mask); median of 5 runs.
+sample of the same frames, one frame per thread, threads = all host cores (the affinity mask,
+SURVEY.md §8(d)), with the same measurement at the per-GPU CPU share (OMP_NUM_THREADS, 16 on the
+GPU box) beside it and the cgroup CPU quota stated; median of 5 runs.
 """
 from __future__ import annotations
 
@@ -57,6 +59,8 @@ WORKLOADS = {
     "uhd4": {"kind": "fixtures", "fixtures": UHD, "width": 3840, "height": 2160, "frames": 512},
     "fhd4": {"kind": "fixtures", "fixtures": FHD, "width": 1920, "height": 1080, "frames": 2048},
     "synth": {"kind": "synth", "width": 3840, "height": 2160, "frames": 512, "seed": 0x5EED, "profile": 0},
+    # BASELINE configs[1] semantics (-yuv, m06 only: no loop filter) on the uhd4 batch
+    "uhd4_yuv": {"kind": "fixtures", "fixtures": UHD, "width": 3840, "height": 2160, "frames": 512, "unfiltered": True},
 }
 FIXTURES = UHD  # (back-compat name used by tools/)
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
@@ -76,7 +80,7 @@ def parse(argv=None):
     ap.add_argument("--unfiltered", action="store_true", help="-yuv semantics (m06 only)")
     ap.add_argument("--waves", type=int, default=0, help="waves per frame workgroup (0 = default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = this process's CPU share")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all host cores for the CPU baseline (and the per-GPU share beside it)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length (all repeats)")
     ap.add_argument("--e2e-frames", type=int, default=256,
                     help="frames of the end-to-end object (.webp bytes -> I420, vp8g_decode_webp_batch); 0 = off")
@@ -154,7 +158,7 @@ class Rank:
         import vp8g_dist
         self.name, self.wl = name, WORKLOADS[name]
         wl = self.wl
-        self.filtered = not args.unfiltered
+        self.filtered = not (args.unfiltered or wl.get("unfiltered", False))
         key = "yuvf" if self.filtered else "yuv"
         n = args.frames or wl["frames"]
         self.lo, self.hi = vp8g_dist.shard_range(n * world, rank, world)
@@ -241,11 +245,23 @@ def timed(launch, steps, warmup, dist, dev):
     return elapsed, kern
 
 
-def cpu_baseline(frames, filtered, threads, seconds, repeats=5):
-    """The reference's m06+m07 (or our restatement) on `frames` round-robin, one frame per thread;
-    median MP/s of `repeats` runs sized to ~seconds in total."""
+def all_cores() -> int:
+    """Every CPU this process may run on (the CPU baseline uses all host cores)."""
+    return len(os.sched_getaffinity(0))
+
+
+def cgroup_cpu_quota():
+    """CPUs' worth of time the cgroup grants this process (cgroup v2 cpu.max), None if unlimited."""
+    try:
+        q, p = pathlib.Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        return None if q == "max" else round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        return None
+
+
+def _cpu_rate(frames, filtered, threads, seconds, repeats, kind):
+    """Median MP/s of `repeats` runs of the CPU path at `threads`, sized to ~seconds in total."""
     import vp8g
-    kind = "reference" if vp8g.ref_available() else "port"
     t = vp8g.cpu_time_batch(frames, threads, threads, filtered, kind)  # calibration, one frame per thread
     if t <= 0:
         return None
@@ -258,12 +274,33 @@ def cpu_baseline(frames, filtered, threads, seconds, repeats=5):
             return None
         rates.append(n * frames[0].width * frames[0].height / 1e6 / t)
         tot += t
+    return statistics.median(rates), n, tot
+
+
+def cpu_baseline(frames, filtered, threads, seconds, repeats=5, share=None):
+    """The reference's m06+m07 (or our restatement) on `frames` round-robin, one frame per thread;
+    median MP/s of `repeats` runs sized to ~seconds in total.  `threads` is the headline thread
+    count (all host cores by default); when `share` differs (the per-GPU share the box grants,
+    OMP_NUM_THREADS), the same measurement at that count is reported beside it."""
+    import vp8g
+    kind = "reference" if vp8g.ref_available() else "port"
+    main = _cpu_rate(frames, filtered, threads, seconds, repeats, kind)
+    if main is None:
+        return None
+    rate, n, tot = main
     w, h = frames[0].width, frames[0].height
-    return {"value": round(statistics.median(rates), 2), "unit": "MP/s", "cores": threads, "kind": kind,
-            "host_cpus": len(os.sched_getaffinity(0)), "cpu_model": cpu_model(),
-            "sample": f"{repeats} x {n} {w}x{h} frames ({len(frames)} distinct, round-robin), one frame per thread, "
-                      f"{'recon+LF (-yuvf)' if filtered else 'recon (-yuv)'} on pre-decoded input, median of "
-                      f"{repeats}, {tot:.1f} s"}
+    obj = {"value": round(rate, 2), "unit": "MP/s", "cores": threads, "kind": kind,
+           "host_cpus": all_cores(), "cgroup_cpu_quota": cgroup_cpu_quota(), "cpu_model": cpu_model(),
+           "sample": f"{repeats} x {n} {w}x{h} frames ({len(frames)} distinct, round-robin), one frame per thread, "
+                     f"{threads} threads, {'recon+LF (-yuvf)' if filtered else 'recon (-yuv)'} on pre-decoded "
+                     f"input, median of {repeats}, {tot:.1f} s"}
+    if share and share != threads:
+        sub = _cpu_rate(frames, filtered, share, seconds, repeats, kind)
+        if sub is not None:
+            obj["share"] = {"value": round(sub[0], 2), "cores": share,
+                            "sample": f"{repeats} x {sub[1]} frames at {share} threads (OMP_NUM_THREADS, the "
+                                      f"per-GPU CPU share), {sub[2]:.1f} s"}
+    return obj
 
 
 def run_workload(name, args, rank, world, dist, dev, golden, rank_factory=Rank):
@@ -334,7 +371,8 @@ def run_workload(name, args, rank, world, dist, dev, golden, rank_factory=Rank):
             obj["roofline"]["traffic"] = tj.get("hbm_bytes_per_launch")
     if rank == 0 and world == 1 and not args.no_cpu_baseline and r.cpu_frames:
         secs = args.cpu_seconds if name == args.workload else args.cpu_seconds / 2
-        obj["cpu_baseline"] = cpu_baseline(r.cpu_frames, r.filtered, args.cpu_threads or cpu_share(), secs)
+        obj["cpu_baseline"] = cpu_baseline(r.cpu_frames, r.filtered, args.cpu_threads or all_cores(), secs,
+                                           share=None if args.cpu_threads else cpu_share())
     return obj
 
 
@@ -451,29 +489,40 @@ def end_to_end(manifest, n_frames, filtered, threads):
            "reference_cli": None}
     dec = ROOT / "oracle" / "_ref" / "decoder"
     if dec.exists():
-        import tempfile
-        from concurrent.futures import ThreadPoolExecutor
-        n_ref = 8 * threads
-        with tempfile.TemporaryDirectory() as td:
-            src = [pathlib.Path(td) / f"f{i}.webp" for i in range(4)]
-            for i in range(4):
-                src[i].write_bytes(files[i])
-
-            def one(i):
-                o = pathlib.Path(td) / f"o{i}.yuv"
-                rc = subprocess.run([str(dec), "-yuvf" if filtered else "-yuv", str(src[i % 4]), str(o)],
-                                    capture_output=True).returncode
-                o.unlink(missing_ok=True)
-                return rc
-            t = time.perf_counter()
-            with ThreadPoolExecutor(threads) as ex:
-                rcs = list(ex.map(one, range(n_ref)))
-            rdt = time.perf_counter() - t
-        if all(rc == 0 for rc in rcs):
-            obj["reference_cli"] = {"value": round(n_ref * 3840 * 2160 / 1e6 / rdt, 1), "unit": "MP/s", "cores": threads,
-                                    "sample": f"{n_ref} x `decoder -yuvf` (reference, one process per frame, {threads} at a "
-                                              f"time), {rdt:.1f} s"}
+        # the reference's own CLI, one process per frame: at the per-GPU share and on all host cores
+        obj["reference_cli"] = reference_cli(dec, files, filtered, threads, 8)
+        if all_cores() != threads:
+            obj["reference_cli_all_cores"] = reference_cli(dec, files, filtered, all_cores(), 2)
     return obj
+
+
+def reference_cli(dec, files, filtered, threads, per_thread):
+    """`decoder -yuvf` of the reference (oracle/_ref/decoder), one process per 4K frame, `threads` at a
+    time, `per_thread` frames per thread (bounded sample); MP/s over the wall clock."""
+    import tempfile
+    from concurrent.futures import ThreadPoolExecutor
+    n_ref = per_thread * threads
+    with tempfile.TemporaryDirectory() as td:
+        src = [pathlib.Path(td) / f"f{i}.webp" for i in range(len(files))]
+        for p, b in zip(src, files):
+            p.write_bytes(b)
+
+        def one(i):
+            o = pathlib.Path(td) / f"o{i}.yuv"
+            rc = subprocess.run([str(dec), "-yuvf" if filtered else "-yuv", str(src[i % len(src)]), str(o)],
+                                capture_output=True).returncode
+            o.unlink(missing_ok=True)
+            return rc
+        t = time.perf_counter()
+        with ThreadPoolExecutor(threads) as ex:
+            rcs = list(ex.map(one, range(n_ref)))
+        rdt = time.perf_counter() - t
+    if not all(rc == 0 for rc in rcs):
+        return None
+    return {"value": round(n_ref * 3840 * 2160 / 1e6 / rdt, 1), "unit": "MP/s", "cores": threads,
+            "cgroup_cpu_quota": cgroup_cpu_quota(),
+            "sample": f"{n_ref} x `decoder -{'yuvf' if filtered else 'yuv'}` (reference, one process per frame, "
+                      f"{threads} at a time), {rdt:.1f} s"}
 
 
 def public(obj: dict) -> dict:

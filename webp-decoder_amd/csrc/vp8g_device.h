@@ -9,20 +9,29 @@ namespace vp8g {
 
 // Per-half-wave LDS scratch (bytes).  A wave works on two macroblocks at once, one per 32-lane
 // half; each half owns one of these areas.  16-B aligned where a 16-B access is made.
-constexpr int kTP = 40;       // tile row pitch: 10 dwords, so that 16 consecutive rows (the lanes of
-                              // a vertical-edge or block pass) fall on 16 different LDS banks
-constexpr int kLfY = 0;       // luma filter tile: 20 rows x kTP (4 rows above + 16 MB rows; two MB
-                              // columns as a ring at +0 / +16, slot = mb_col & 1)
-constexpr int kLfUV = 800;    // chroma tile: 12 rows x kTP (4 above + 8 MB rows); per row U at +0,
-                              // V at +16, each a ring of two 8-B MB columns
-constexpr int kAbY = 1280;    // luma above row: [15] corner P, [16..31] A, [32..35] above-right
-constexpr int kAbUV = 1328;   // chroma above rows: U P@7 A@8..15, V P@23 A@24..31
-constexpr int kColY = 1360;   // B_PRED: luma columns 11, 7, 3 of the MB (16 B each, in that order),
-                              // so that the left column of sub-block column j is at kLeft - 16 j
-constexpr int kLeft = 1408;   // unfiltered left columns: Y 0..15, U 16..23, V 24..31
-constexpr int kResid = 1440;  // luma residual of the MB (for B_PRED): 16 blocks x 16 int16
-constexpr int kWht = 1952;    // 16 int16 luma DCs out of the inverse WHT
-constexpr int kHalfBytes = 1984;
+// The loop filter runs one macroblock behind reconstruction (MB c is reconstructed while MB c - 1
+// is filtered, and the MB edge of c - 1 reaches 4 pixels into c - 2), so the filter tiles are a
+// ring of three MB columns, slot = mb_col mod 3.
+constexpr int kRing = 3;
+constexpr int kTP = 56;       // tile row pitch (luma and chroma: the horizontal-edge pass reads both
+                              // planes' lines with one set of immediate row offsets)
+constexpr int kCV = 24;       // chroma tile: V plane offset in a row (U at +0), each a ring of 3 x 8 B
+constexpr int kLfY = 0;       // luma filter tile: 20 rows x kTP (4 rows above + 16 MB rows; three MB
+                              // columns as a ring at +0 / +16 / +32)
+// chroma tile: 12 rows x kTP (4 above + 8 MB rows), 4 bytes off 8-B alignment: with luma rows 14
+// dwords apart, the 32 lines of a half's vertical-edge pass (16 luma, 8 U, 8 V rows) then meet at
+// most 2 per LDS bank, the horizontal-edge pass mostly 1 (a 2-way conflict in one slot of three):
+// tools/lds_banks.py.  (Chroma 8-B pieces are therefore accessed as two dwords.)
+constexpr int kLfUV = 20 * kTP + 4;
+constexpr int kAbY = (kLfUV + 12 * kTP + 15) & ~15;  // luma above row: [15] corner P, [16..31] A, [32..35] above-right
+constexpr int kAbUV = kAbY + 48;  // chroma above rows: U P@7 A@8..15, V P@23 A@24..31
+constexpr int kColY = kAbUV + 32; // B_PRED: luma columns 11, 7, 3 of the MB (16 B each, in that order),
+                                  // so that the left column of sub-block column j is at kLeft - 16 j
+constexpr int kLeft = kColY + 48; // unfiltered left columns: Y 0..15, U 16..23, V 24..31
+constexpr int kResid = kLeft + 32;  // luma residual of the MB (for B_PRED): 16 blocks x 16 int16
+constexpr int kWht = kResid + 512;  // 16 int16 luma DCs out of the inverse WHT
+constexpr int kHalfBytes = kWht + 32;
+static_assert(kAbY % 16 == 0 && kColY % 16 == 0 && kLeft % 16 == 0 && kResid % 16 == 0, "16-B aligned areas");
 constexpr int kWaveBytes = 2 * kHalfBytes;
 
 // Workgroup header.
