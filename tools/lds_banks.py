@@ -7,12 +7,15 @@ horizontal-edge pass with one lane per pixel COLUMN (immediate row offsets, so l
 the tile pitch).  A 32-lane group of a wave64 LDS instruction costs one LDS cycle per distinct dword
 on its busiest bank (MI355X_MICROARCH.md, LDS: bank = dword mod 32 for 4-byte-and-smaller accesses;
 lanes reading the same dword broadcast).  This prints the cost of the 20 gather instructions of each
-pass for every ring slot, for the shipped layout (vp8g_device.h: kTP, kLfUV, kCV) and, with
---search, the best layouts within the LDS budget of two 4K frames per CU.
+pass for every ring slot, for the shipped layout (vp8g_device.h: kTP, kLfUV, kCV; two-column
+ring) and for the three-column ring of the loop-filter-behind experiment, and, with --search, the
+best layouts within the LDS budget of two 4K frames per CU.
 
-Measured (tools/ab_inproc.py, 512 x 4K, one box): the same lagged kernel with pitch 52 / chroma at
-20 * 52 (vertical pass 2-3-way, horizontal 1-2-way) 15.58 ms; pitch 56 / chroma at 20 * 56 + 4
-(vertical 2-way, horizontal 1-way in two slots of three) 14.47 ms.
+Measured (tools/ab_inproc.py, 512 x 4K, one box; profiles/r03_ab_lf_behind.json): round-2 layout
+(pitch 40, chroma at 800: vertical pass 3-way) 14.40 ms, chroma at 804 (2-way) 14.26 ms; the
+three-column ring at pitch 52 15.58 ms, at pitch 56 / chroma + 4 14.47 ms.  The model ranks bank
+conflicts only: pitches that are not a multiple of 8 also split the 8-B luma row accesses (pitch 52
+lost 2-3 % whatever its bank score).
 
   python tools/lds_banks.py [--search]
 """
@@ -62,9 +65,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--search", action="store_true")
     a = ap.parse_args()
-    print("shipped: pitch 56, chroma at 20*56+4, V at +24, 3-slot ring")
+    print("shipped: pitch 40, chroma at 804, V at +16, 2-slot ring")
+    report(40, 804, 16, 2)
+    print("round 2: pitch 40, chroma at 800, V at +16, 2-slot ring")
+    report(40, 800, 16, 2)
+    print("loop filter one MB behind (be261fe): pitch 56, chroma at 20*56+4, V at +24, 3-slot ring")
     report(56, 20 * 56 + 4, 24)
-    print("pitch 52, chroma at 20*52, V at +24 (first lagged build)")
+    print("pitch 52, chroma at 20*52, V at +24, 3-slot ring (first lagged build)")
     report(52, 20 * 52, 24)
     if a.search:
         best = []

@@ -9,29 +9,36 @@ namespace vp8g {
 
 // Per-half-wave LDS scratch (bytes).  A wave works on two macroblocks at once, one per 32-lane
 // half; each half owns one of these areas.  16-B aligned where a 16-B access is made.
-// The loop filter runs one macroblock behind reconstruction (MB c is reconstructed while MB c - 1
-// is filtered, and the MB edge of c - 1 reaches 4 pixels into c - 2), so the filter tiles are a
-// ring of three MB columns, slot = mb_col mod 3.
-constexpr int kRing = 3;
-constexpr int kTP = 56;       // tile row pitch (luma and chroma: the horizontal-edge pass reads both
-                              // planes' lines with one set of immediate row offsets)
-constexpr int kCV = 24;       // chroma tile: V plane offset in a row (U at +0), each a ring of 3 x 8 B
-constexpr int kLfY = 0;       // luma filter tile: 20 rows x kTP (4 rows above + 16 MB rows; three MB
-                              // columns as a ring at +0 / +16 / +32)
-// chroma tile: 12 rows x kTP (4 above + 8 MB rows), 4 bytes off 8-B alignment: with luma rows 14
-// dwords apart, the 32 lines of a half's vertical-edge pass (16 luma, 8 U, 8 V rows) then meet at
-// most 2 per LDS bank, the horizontal-edge pass mostly 1 (a 2-way conflict in one slot of three):
-// tools/lds_banks.py.  (Chroma 8-B pieces are therefore accessed as two dwords.)
-constexpr int kLfUV = 20 * kTP + 4;
+// Filter tiles (luma 20 rows, chroma 12 rows, one pitch: the horizontal-edge pass reads every
+// plane's lines with one set of immediate row offsets), each row a ring of two MB columns (slot =
+// mb_col & 1).  Their placement sets the LDS bank conflicts of the loop filter's byte gathers
+// (tools/lds_banks.py): 32 lines per 32-lane half -- 16 luma, 8 U and 8 V rows in the vertical-edge
+// pass -- should spread over the 32 banks.  With the chroma tile 4 bytes off 8-B alignment the
+// chroma 8-B pieces are accessed as two dwords (kC8).
+#ifndef VP8G_TP
+#define VP8G_TP 40
+#endif
+#ifndef VP8G_UV
+#define VP8G_UV 804
+#endif
+#ifndef VP8G_CV
+#define VP8G_CV 16
+#endif
+constexpr int kTP = VP8G_TP;    // tile row pitch
+constexpr int kLfY = 0;         // luma filter tile: 20 rows x kTP (4 rows above + 16 MB rows; two MB
+                                // columns as a ring at +0 / +16)
+constexpr int kLfUV = VP8G_UV;  // chroma tile: 12 rows x kTP (4 above + 8 MB rows); per row U at +0,
+constexpr int kCV = VP8G_CV;    // V at +kCV, each a ring of two 8-B MB columns
+constexpr bool kC8 = kLfUV % 8 == 0 && kTP % 8 == 0 && kCV % 8 == 0;  // chroma 8-B pieces 8-B aligned
+static_assert(kLfUV >= 20 * kTP && kCV >= 16 && kCV + 16 <= kTP, "tile layout");
 constexpr int kAbY = (kLfUV + 12 * kTP + 15) & ~15;  // luma above row: [15] corner P, [16..31] A, [32..35] above-right
-constexpr int kAbUV = kAbY + 48;  // chroma above rows: U P@7 A@8..15, V P@23 A@24..31
-constexpr int kColY = kAbUV + 32; // B_PRED: luma columns 11, 7, 3 of the MB (16 B each, in that order),
-                                  // so that the left column of sub-block column j is at kLeft - 16 j
-constexpr int kLeft = kColY + 48; // unfiltered left columns: Y 0..15, U 16..23, V 24..31
+constexpr int kAbUV = kAbY + 48;   // chroma above rows: U P@7 A@8..15, V P@23 A@24..31
+constexpr int kColY = kAbUV + 32;  // B_PRED: luma columns 11, 7, 3 of the MB (16 B each, in that order),
+                                   // so that the left column of sub-block column j is at kLeft - 16 j
+constexpr int kLeft = kColY + 48;  // unfiltered left columns: Y 0..15, U 16..23, V 24..31
 constexpr int kResid = kLeft + 32;  // luma residual of the MB (for B_PRED): 16 blocks x 16 int16
 constexpr int kWht = kResid + 512;  // 16 int16 luma DCs out of the inverse WHT
 constexpr int kHalfBytes = kWht + 32;
-static_assert(kAbY % 16 == 0 && kColY % 16 == 0 && kLeft % 16 == 0 && kResid % 16 == 0, "16-B aligned areas");
 constexpr int kWaveBytes = 2 * kHalfBytes;
 
 // Workgroup header.

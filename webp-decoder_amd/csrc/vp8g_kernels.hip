@@ -220,9 +220,15 @@ DEV uint32_t ld32(const uint8_t* p) { return *(const uint32_t*)p; }
 DEV void st32(uint8_t* p, uint32_t v) { *(uint32_t*)p = v; }
 DEV u32x2 ld64(const uint8_t* p) { return *(const u32x2*)p; }
 DEV void st64(uint8_t* p, u32x2 v) { *(u32x2*)p = v; }
-// 8 bytes at a 4-B aligned LDS address (the chroma tile)
-DEV u32x2 ld64u(const uint8_t* p) { return u32x2{ld32(p), ld32(p + 4)}; }
-DEV void st64u(uint8_t* p, u32x2 v) { st32(p, v.x), st32(p + 4, v.y); }
+// a chroma tile 8-B piece (4-B aligned unless kC8)
+DEV u32x2 ldc64(const uint8_t* p) {
+	if constexpr (kC8) return ld64(p);
+	else return u32x2{ld32(p), ld32(p + 4)};
+}
+DEV void stc64(uint8_t* p, u32x2 v) {
+	if constexpr (kC8) st64(p, v);
+	else st32(p, v.x), st32(p + 4, v.y);
+}
 DEV u32x4 ld128(const uint8_t* p) { return *(const u32x4*)p; }
 DEV void st128(uint8_t* p, u32x4 v) { *(u32x4*)p = v; }
 DEV uint32_t pack4(int a, int b, int c, int d) {
@@ -448,24 +454,23 @@ DEV void gather20(const uint8_t* a, const uint8_t* b, int* px) {
 	for (int i = 0; i < 20; i++) __builtin_assume((uint32_t)px[i] < 256u);  // bytes: lets 24-bit multiplies through
 }
 
-// Both passes of the loop filter over this lane's line of the MB held in LDS (ring slot `slot`;
-// its left neighbour in ring slot `nslot`).  Lanes 0..15: luma rows / columns; 16..23 U, 24..31 V.
-// Bytes that may change: 1..17 (luma), 1..9 (chroma).
+// Both passes of the loop filter over this lane's line of the MB held in LDS.  Lanes 0..15:
+// luma rows / columns; 16..23 U, 24..31 V.  Bytes that may change: 1..17 (luma), 1..9 (chroma).
 template <bool kSimple>
-DEV void lf_mb(uint8_t* tY, uint8_t* tC, int ln, int slot, int nslot, bool en, bool mb_v, bool mb_h, bool inner, int E, int I,
-               int T) {
+DEV void lf_mb(uint8_t* tY, uint8_t* tC, int ln, int slot, bool en, bool mb_v, bool mb_h, bool inner, int E, int I, int T) {
 	const bool isy = ln < 16;
 	const int cp = (ln >> 3) & 1;
 	const bool wr = en && (isy || !kSimple);
 	int px[20];
-	// vertical edges: one line per lane along a pixel row; the neighbour's last 4 pixels sit in its
-	// own ring slot
+	// vertical edges: one line per lane along a pixel row; the neighbour's 4 pixels sit at the
+	// other end of the 2-MB ring when slot == 0
 	{
 		// (ldb/stb: relaxed wave-scope atomics keep the byte accesses single ds_read_u8 /
 		// ds_write_b8 -- merged wide accesses cost vector instructions to (un)pack)
 		uint8_t* const rowp = isy ? tY + (4 + ln) * kTP : tC + (4 + (ln & 7)) * kTP + cp * kCV;
-		uint8_t* const Lp = rowp + (isy ? nslot * 16 + 12 : nslot * 8 + 4);
-		uint8_t* const Mp = rowp + (isy ? slot * 16 : slot * 8);
+		const int off = isy ? slot * 16 : slot * 8, ring = isy ? 31 : 15;
+		uint8_t* const Lp = rowp + ((off - 4) & ring);
+		uint8_t* const Mp = rowp + off;
 		PRIO(8);
 		gather20<1, 1>(Lp, Mp, px);
 		PRIO(9);
@@ -617,11 +622,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 	ctx.lds = smem + kHdrBytes + NW * kWaveBytes;
 	ctx.g = kG ? gctx + (size_t)f * ctx_cols * kCtxBytesPerCol : nullptr;
 	const uint32_t npairs = (R + 1) >> 1;
-	// Loop-filtered frames filter MB c - 1 while MB c is reconstructed: one more step per row.
-	// A pair's steps: the upper row's C (+ 1) and the lower row's 2-column skew; CPS is also the
-	// stride of the progress words (pair * CPS + steps done).
-	const uint32_t lag1 = (flags & VP8G_F_LOOPFILTER) ? 1u : 0u;
-	const uint32_t CPS = C + 2 + lag1;
+	const uint32_t CP2 = C + 2;
 	const uint32_t GW = K * NW, gw = part * NW + (uint32_t)wave;
 	const size_t chan = (size_t)ctx_cols * kCtxBytesPerCol;
 	const uint32_t pin = (part + K - 1) % K;  // the part holding this part's wave-0 predecessors
@@ -665,7 +666,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 		u32x4 mbx = u32x4{0u, 0u, 0u, 0u};                     // mailbox prefetch (xin: lanes 0..9)
 		const uint32_t rA = 2 * k;
 		const bool two = rA + 1 < R;
-		const uint32_t T = (two ? C + 2 : C) + lag1;
+		const uint32_t T = two ? CP2 : C;
 		// Per-lane row bases of this pair (lane roles: ln 0..24 one 32-B coefficient block each --
 		// Y 0..15, U 16..19, V 20..23, Y2 24 (and 26..31, duplicates) -- ln 25 the 16 B_PRED modes;
 		// side bytes ln&3: ymode, uv_mode, segment_id, has_coeff for lanes 26..29).  MB m's data
@@ -715,12 +716,8 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 		// prefetched data waits for the loads alone, never for stores (see kNoStore)
 		bst128(rY, kNoStore, u32x4{0u, 0u, 0u, 0u});
 		bst64(rC, kNoStore, u32x2{0u, 0u});
-		// loop-filter parameters of this half's previous MB (the one filtered this step):
-		// [7:0] offset of its row in the LF table (segment, B_PRED), bit 8 inner edges
-		uint32_t lfi_prev = 0;
-		uint32_t t3 = 0;  // t mod 3 (ring slot of the upper row's MB)
 
-		for (uint32_t t = 0; t < T; t++, t3 = t3 == 2u ? 0u : t3 + 1u) {
+		for (uint32_t t = 0; t < T; t++) {
 			// Lane-derived values are recomputed every step from a laundered lane id: hoisting the
 			// lane-dependent LDS addresses out of the loop would exhaust the VGPR budget.
 			int lane = lane0;
@@ -737,18 +734,9 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			const int hh = lane >> 5, ln = lane & 31;
 			const uint32_t r = rA + (uint32_t)hh;
 			const int c = (int)t - 2 * hh;
-			const bool rowv = hh == 0 || two;
-			const bool act = rowv && c >= 0 && c < (int)C;  // reconstructs MB(r, c) this step
+			const bool act = (hh == 0 || two) && c >= 0 && c < (int)C;
 			const uint32_t cu = (uint32_t)c;
-			// the MB filtered this step: lc = c - 1 (loop-filtered frames; else c itself)
-			const int lc = c - (int)lag1;
-			const uint32_t lcu = (uint32_t)lc;
-			const bool lact = rowv && lc >= 0 && lc < (int)C;
-			// ring slots (c mod 3) of MB c, of the filtered MB and of its left neighbour
-			const uint32_t t3n = t3 == 2u ? 0u : t3 + 1u, t3p = t3 == 0u ? 2u : t3 - 1u;
-			const int slot = (int)(hh ? t3n : t3);                                   // (t - 2) mod 3 = (t + 1) mod 3
-			const int lslot = lag1 ? (int)(hh ? t3 : t3p) : slot;                    // (c - 1) mod 3
-			const int nslot = lag1 ? (int)(hh ? t3p : t3n) : (int)(hh ? t3 : t3p);  // (lc - 1) mod 3
+			const int slot = c & 1;
 			uint8_t* const hv = smem + kHdrBytes + wave * kWaveBytes + (hh ? kHalfBytes : 0);  // this half's area
 			uint8_t* const tY = hv + kLfY;
 			uint8_t* const tC = hv + kLfUV;  // chroma: U at +0, V at +kCV, row pitch kTP
@@ -867,7 +855,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			if (k > 0 && !dead && !(VP8G_ABLATE & 8)) {
 				// (one column more lag across parts: the mailbox is read a step ahead of use)
 				const uint32_t lag = xin ? 5u : 4u;
-				const uint32_t need = (k - 1) * CPS + ((t + lag < CPS) ? t + lag : CPS);
+				const uint32_t need = (k - 1) * CP2 + ((t + lag < CP2) ? t + lag : CP2);
 				const uint32_t pw = (uint32_t)((wave + NW - 1) % NW);
 				uint32_t spins = 0;
 				uint64_t t0 = 0;
@@ -887,10 +875,9 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 				asm volatile("" ::: "memory");
 			}
 			if (kS && xin) {
-				// mailbox -> this part's LDS ctx: rec[t + 1] and lf[t - lag1] (the column filtered this
-				// step) now, loaded last step (at t = 0 rec[0], rec[1] and, unlagged, lf[0] directly), then
-				// the loads for the next step (lane roles: ln 0..1 the 32-B rec entry, 2..9 the 128-B lf
-				// entry, as 16-B pieces)
+				// mailbox -> this part's LDS ctx: rec[t + 1] and lf[t] now (loaded last step; at t = 0
+				// rec[0], rec[1], lf[0] directly), then the loads for the next step (lane roles: ln 0..1
+				// the 32-B rec entry, 2..9 the 128-B lf entry, as 16-B pieces)
 				auto mload = [&](uint32_t col, uint32_t o) -> u32x4 {
 					const uint32_t* q = (const uint32_t*)(mb_in + (size_t)col * kCtxBytesPerCol + o);
 					return u32x4{__hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
@@ -900,15 +887,14 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 				};
 				const uint32_t o = 16u * (uint32_t)(lane0 & 15);  // byte offset in the column entry
 				if (t == 0) {
-					// ln 0..1 (+ 2..9 unlagged): column 0 (rec + lf), 10..11: rec of column 1
+					// ln 0..9: column 0 (rec + lf), 10..11: rec of column 1
 					const uint32_t col = lane0 < 10 ? 0u : 1u, oo = lane0 < 10 ? o : o - 160u;
-					const bool want = lane0 < 12 && (lane0 < 2 || lane0 >= 10 || lag1 == 0u) && col < C;
-					if (want) st128(ctx.lds + col * kCtxBytesPerCol + oo, mload(col, oo));
+					if (lane0 < 12 && col < C) st128(ctx.lds + col * kCtxBytesPerCol + oo, mload(col, oo));
 				} else {
-					const uint32_t col = lane0 < 2 ? t + 1 : t - lag1;
+					const uint32_t col = lane0 < 2 ? t + 1 : t;
 					if (lane0 < 10 && col < C) st128(ctx.lds + col * kCtxBytesPerCol + o, mbx);
 				}
-				const uint32_t ncol = lane0 < 2 ? t + 2 : t + 1 - lag1;
+				const uint32_t ncol = lane0 < 2 ? t + 2 : t + 1;
 				if (lane0 < 10 && ncol < C) mbx = mload(ncol, o);
 				wave_lds_sync();
 			}
@@ -929,7 +915,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					} else {
 						const int p = (ln - 16) >> 3, row = ln & 7;
 						const uint8_t* s = src + (p ? D.src_v : D.src_u) + (size_t)(cy0 + row) * D.src_stride_uv + cx0;
-						st64u(tC + p * kCV + (4 + row) * kTP + slot * 8, u32x2{ld32(s), ld32(s + 4)});
+						stc64(tC + p * kCV + (4 + row) * kTP + slot * 8, u32x2{ld32(s), ld32(s + 4)});
 					}
 				} else {
 					// One 4-byte store per lane 0..19 (kBorderTab: destination, context source, kind):
@@ -950,16 +936,14 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					const uint32_t v = kind == 0 ? vabove : (kind == 1 ? 0x81818181u : vcorner);
 					if (ln < 20 && (kind != 1 || c == 0)) st32(hv + (bt & 0xFFFu), v);
 				}
-			}
-			if (lf_on && lact && r > 0 && ln >= 20) {
-				// filter state of the MB above the MB filtered this step (both modes), final since the
-				// row above filtered column lc + 1
-				const bool ly = ln < 24;
-				const int p = (ln - 24) >> 2, tr = ly ? ln - 20 : (ln - 24) & 3;
-				const uint32_t lo = lf_off(lcu) + (ly ? tr * 16 : 64 + p * 32 + tr * 8);
-				uint8_t* const td = ly ? tY + tr * kTP + lslot * 16 : tC + p * kCV + tr * kTP + lslot * 8;
-				if (ly) st64(td, ctx.rd64(lo)), st64(td + 8, ctx.rd64(lo + 8));
-				else st64u(td, ctx.rd64(lo));
+				if (lf_on && !top && ln >= 20) {  // filter state of the MB above (both modes)
+					const bool ly = ln < 24;
+					const int p = (ln - 24) >> 2, tr = ly ? ln - 20 : (ln - 24) & 3;
+					const uint32_t lo = lf_off(cu) + (ly ? tr * 16 : 64 + p * 32 + tr * 8);
+					uint8_t* const td = ly ? tY + tr * kTP + slot * 16 : tC + p * kCV + tr * kTP + slot * 8;
+					if (ly) st64(td, ctx.rd64(lo)), st64(td + 8, ctx.rd64(lo + 8));
+					else stc64(td, ctx.rd64(lo));
+				}
 			}
 			wave_lds_sync();
 			STAMP(2);
@@ -1102,22 +1086,18 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			// corner for the next MB is taken at its border setup)
 			STAMP(4);
 
-			// ---------------------------------------------- loop filter MB(r, c - 1)
+			// ---------------------------------------------- loop filter MB(r, c)
 			PRIO(5);
-			// MB c's filter parameters (LF table row: segment, B_PRED; inner edges when it has
-			// coefficients or is B_PRED), used next step when MB c is filtered
-			const uint32_t lfi_cur = (uint32_t)(seg * 8 + (bpred ? 4 : 0)) | ((hasc != 0 || bpred) ? 256u : 0u);
 			if (lf_on && !(VP8G_ABLATE & 1)) {
-				const uint8_t* lp = smem + kLfTable + (lfi_prev & 0xFFu);
+				const uint8_t* lp = smem + kLfTable + seg * 8 + (bpred ? 4 : 0);
 				const int E = lp[0], I = lp[1], Tt = lp[2];
-				const bool en = lact && E != 0;
+				const bool en = act && E != 0;
 				if (__ballot(en) != 0ull) {
-					const bool inner = (lfi_prev & 256u) != 0u;
-					if (simple) lf_mb<true>(tY, tC, ln, lslot, nslot, en, lc > 0, r > 0, inner, E, I, Tt);
-					else lf_mb<false>(tY, tC, ln, lslot, nslot, en, lc > 0, r > 0, inner, E, I, Tt);
+					const bool inner = hasc != 0 || bpred;
+					if (simple) lf_mb<true>(tY, tC, ln, slot, en, c > 0, r > 0, inner, E, I, Tt);
+					else lf_mb<false>(tY, tC, ln, slot, en, c > 0, r > 0, inner, E, I, Tt);
 				}
 			}
-			lfi_prev = lfi_cur;
 			STAMP(5);
 
 			// ---------------------------------------------- store final pixels
@@ -1168,7 +1148,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 				srcY = tY + (4 + (ln & 15)) * kTP + slot * 16;
 				const int p = (ln >> 3) & 1, row = ln & 7;
 				srcC = tC + p * kCV + (4 + row) * kTP + slot * 8;
-				yl0 = ld64(srcY), yl1 = ld64(srcY + 8), cl0 = ld64u(srcC);
+				yl0 = ld64(srcY), yl1 = ld64(srcY + 8), cl0 = ldc64(srcC);
 				{
 					const uint32_t colpx = cu * 16u, prow = y0 + (uint32_t)(ln & 15);
 					const uint32_t off = __umul24(prow, sy) + colpx;
@@ -1186,13 +1166,12 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					poffC = off, pcntC = vis && !full ? min(CW - colpx, 8u) : 0u;
 				}
 			} else {
-				// (after filtering MB lc = c - 1: the MB above it and its left neighbour are final)
-				{  // luma: ln 0..3 the bottom rows of the MB above MB lc; 4..19 the MB left of it
+				{  // luma: ln 0..3 the MB above's bottom rows (this column, final now); 4..19 the left MB
 					const bool top = ln < 4;
-					const uint32_t col = top ? lcu : lcu - 1;
-					srcY = tY + ln * kTP + (top ? lslot : nslot) * 16;
+					const uint32_t col = top ? cu : cu - 1;
+					srcY = tY + ln * kTP + (top ? slot : slot ^ 1) * 16;
 					yl0 = ld64(srcY), yl1 = ld64(srcY + 8);
-					const bool ok = lact && (fl_bits & 1u) && (top || lc > 0);
+					const bool ok = act && (fl_bits & 1u) && (top || c > 0);
 					const bool to_ctx = ok && (fl_bits & 2u);
 					if (to_ctx) ctx.wr128(lf_off(col) + (ln - 16) * 16, u32x4{yl0.x, yl0.y, yl1.x, yl1.y});
 #if VP8G_ABLATE & 16  // diagnostic: same stores, linearised per half (whole lines; output wrong)
@@ -1209,10 +1188,10 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 				{  // chroma: plane ln / 12, tile row ln % 12 (same split)
 					const int p = ln >= 12 ? 1 : 0, kr = ln - 12 * p;
 					const bool top = kr < 4;
-					const uint32_t col = top ? lcu : lcu - 1;
-					srcC = tC + p * kCV + kr * kTP + (top ? lslot : nslot) * 8;
-					cl0 = ld64u(srcC);
-					const bool ok = lact && (fl_bits & 8u) && (top || lc > 0);
+					const uint32_t col = top ? cu : cu - 1;
+					srcC = tC + p * kCV + kr * kTP + (top ? slot : slot ^ 1) * 8;
+					cl0 = ldc64(srcC);
+					const bool ok = act && (fl_bits & 8u) && (top || c > 0);
 					const bool to_ctx = ok && (fl_bits & 16u);
 					if (to_ctx) ctx.wr64(lf_off(col) + 64 + p * 32 + (kr - 8) * 8, cl0);
 #if VP8G_ABLATE & 16
@@ -1247,16 +1226,16 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 				};
 				auto flushC = [&](bool ok, int p, int trow, uint32_t col, int sl) {
 					const uint8_t* src = tC + p * kCV + trow * kTP + sl * 8;
-					const u32x2 lo = ld64u(src);
+					const u32x2 lo = ldc64(src);
 					const bool to_ctx = ok && trow >= 8 && !last_row;
 					if (to_ctx) ctx.wr64(lf_off(col) + 64 + p * 32 + (trow - 8) * 8, lo);
 					emitC(ok && !to_ctx, p, cy0 + trow - 4, col, src, lo);
 				};
 				SUBMARK(21);
-				if (__ballot(lact && lcu + 1 == C) != 0ull) {  // last column: its own rows are final too
-					const bool own = lact && lcu + 1 == C;
-					flushY(own && ln < 16, 4 + ln, lcu, lslot);
-					flushC(own && ln < 16, ln >> 3, 4 + (ln & 7), lcu, lslot);
+				if (__ballot(act && cu + 1 == C) != 0ull) {  // last column: its own rows are final too
+					const bool own = act && cu + 1 == C;
+					flushY(own && ln < 16, 4 + ln, cu, slot);
+					flushC(own && ln < 16, ln >> 3, 4 + (ln & 7), cu, slot);
 				}
 			}
 			wave_lds_sync();
@@ -1267,9 +1246,9 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			ctx.publish_fence();
 			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 			if (kS && xout) {
-				// the ctx entries this step finished (rec of column t - 2, lf of column t - 3 - lag1, and at
-				// the last step lf of column C - 1) -> mailbox, write-through; drained before the flag
-				const int cl = lane0 < 2 ? (int)t - 2 : (lane0 < 10 ? (int)t - 3 - (int)lag1 : (t + 1 == T ? (int)C - 1 : -1));
+				// the ctx entries this step finished (rec of column t - 2, lf of column t - 3, and at the
+				// last step lf of column C - 1) -> mailbox, write-through; drained before the flag
+				const int cl = lane0 < 2 ? (int)t - 2 : (lane0 < 10 ? (int)t - 3 : (t + 1 == T ? (int)C - 1 : -1));
 				const uint32_t o = lane0 < 2 ? 16u * (uint32_t)lane0 : 32u + 16u * (uint32_t)((lane0 - 2) & 7);
 				if (lane0 < 18 && cl >= 0 && cl < (int)C) {
 					const u32x4 v = ld128(ctx.lds + (uint32_t)cl * kCtxBytesPerCol + o);
@@ -1280,10 +1259,10 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					__hip_atomic_store(q + 3, v.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 				}
 				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-				if (lane == 0) __hip_atomic_store(gp_out, k * CPS + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+				if (lane == 0) __hip_atomic_store(gp_out, k * CP2 + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 			}
 			if (lane == 0 && wave != VP8G_TEST_STALL_WAVE)
-				__hip_atomic_store(prog + wave, k * CPS + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+				__hip_atomic_store(prog + wave, k * CP2 + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 			STAMP(7);
 		}
 	}
