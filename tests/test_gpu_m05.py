@@ -177,3 +177,19 @@ def test_pipeline_device_m05_hybrid_split(vp8g, manifest, monkeypatch, hybrid):
     assert st == [0] * len(rels)
     bad = [r for r, o in zip(rels, outs) if sha(o) != manifest["files"][r]["yuvf_sha256"]]
     assert not bad, bad[:8]
+
+
+def test_pipeline_hybrid_small_host_chunks_beside_device_m05(vp8g, manifest, monkeypatch):
+    """host-m05 chunks of 2 frames (which alone would run in split mode) launched while
+    the device-m05 chunk's long kernel runs on another stream.  Chunks of a multi-chunk call never
+    split (their parts could wait on CUs another stream holds), so every frame decodes and matches
+    the reference's -yuvf output."""
+    monkeypatch.setenv("VP8G_HYBRID", "1")
+    monkeypatch.setenv("VP8G_CHUNK_FRAMES", "2")
+    rels = ["big/uhd_d_normal_q90.webp", "big/uhd_a_normal_seg4.webp", "big/fhd_normal_sharp5.webp"] * 4 + \
+        sorted(manifest["files"])[::25]
+    files = [(FIXTURES / r).read_bytes() for r in rels]
+    outs, st = vp8g.gpu_decode_webp_batch(files, True, 4, device_m05=True)
+    assert st == [0] * len(rels)
+    bad = [r for r, o in zip(rels, outs) if sha(o) != manifest["files"][r]["yuvf_sha256"]]
+    assert not bad, bad[:8]

@@ -73,7 +73,9 @@ __host__ __device__ inline uint32_t cost_class(const Vp8gFrameDesc& d) {
 			}
 		if (d.flags & VP8G_F_SIMPLE) s >>= 1;
 	}
-	const uint64_t cost = (uint64_t)d.mb_cols * d.mb_rows * (64u + s);  // >= 64, < 2^30
+	const uint64_t cost = (uint64_t)d.mb_cols * d.mb_rows * (64u + s);  // < 2^27 for valid frames
+	if (cost < 4u) return 0u;  // an empty (all-zero) descriptor: a no-op slot, the lightest class
+	if (cost >= (1ull << 31)) return kCostClasses - 1u;
 	const uint32_t lg = 63u - (uint32_t)__builtin_clzll(cost);
 	return 4u * lg + (uint32_t)((cost >> (lg - 2u)) & 3u);
 }

@@ -548,6 +548,7 @@ DEV uint32_t ordered_frame(const Vp8gFrameDesc* descs, uint32_t n, uint32_t F, u
 	// so the heaviest frame shares its CU with the lightest), the rest the middle, heaviest first
 	const uint32_t p = w < F ? w : (w < F + S ? n - 1u - (w - F) : w - S);
 	for (uint32_t i = tid; i < kCostClasses; i += NT) hist[i] = 0u;
+	if (tid == 0) *found = w < n ? w : 0u;  // (every position is matched; this only keeps the read defined)
 	__syncthreads();
 	for (uint32_t i = tid; i < n; i += NT) atomicAdd(&hist[cost_class(descs[i])], 1u);
 	__syncthreads();

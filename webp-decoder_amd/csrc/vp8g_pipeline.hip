@@ -7,7 +7,7 @@
 //   this thread      groups finished frames into chunks; per chunk: H2D of the side arrays, the
 //                    block masks and the non-zero values (~5x less than dense int16), expansion
 //                    to the dense SoA the recon kernel reads, the fused recon(+LF) kernel, D2H
-//                    into the callers' images.  Two chunk slots alternate, so the device work and
+//                    into the callers' images.  Chunk slots alternate (two per chunk kind), so the device work and
 //                    the copies of one chunk overlap the entropy decoding of the next ones.
 //
 // With VP8G_BATCH_DEVICE_M05 the workers only parse the container, the
@@ -101,6 +101,44 @@ struct TokJob {
 	uint64_t poff;  // VP8 payload in the file
 	uint32_t psize;
 };
+
+// The library's one background releaser of host frames (the last chunks' packed frames, freed
+// after a call returns: see defer_release).  Owned, and joined when the library is unloaded or
+// the process exits, so no thread runs library code after that.
+struct Freer {
+	std::mutex mu;
+	std::condition_variable cv;
+	std::vector<std::vector<Vp8gPackedFrame>> q;
+	bool stop = false;
+	std::thread th;
+	void post(std::vector<Vp8gPackedFrame>&& v) {
+		std::lock_guard<std::mutex> lk(mu);
+		if (!th.joinable()) th = std::thread([this] { run(); });
+		q.push_back(std::move(v));
+		cv.notify_one();
+	}
+	void run() {
+		std::unique_lock<std::mutex> lk(mu);
+		for (;;) {
+			cv.wait(lk, [this] { return stop || !q.empty(); });
+			if (q.empty()) return;  // (stop with nothing queued)
+			std::vector<Vp8gPackedFrame> v = std::move(q.back());
+			q.pop_back();
+			lk.unlock();
+			for (Vp8gPackedFrame& p : v) vp8f_packed_free(&p);
+			lk.lock();
+		}
+	}
+	~Freer() {
+		{
+			std::lock_guard<std::mutex> lk(mu);
+			stop = true;
+		}
+		cv.notify_one();
+		if (th.joinable()) th.join();
+	}
+};
+Freer g_freer;
 
 uint32_t default_threads() {
 	cpu_set_t set;
@@ -370,12 +408,12 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 	}
 	uint64_t chunk_mbs_tok = kTokChunkMbs, chunk_mbs_pk = kChunkMbs;
 	{
-		// two chunk slots of ~1.3 KB per MB each (+ payloads): keep both within ~3/8 of the free
-		// device memory, so a device shared with other work gets smaller chunks instead of a failed
-		// allocation (EIO for every frame)
+		// four chunk slots (two per chunk kind) of ~1.3 KB per MB each (+ payloads): keep all of
+		// them within ~3/8 of the free device memory, so a device shared with other work gets
+		// smaller chunks instead of a failed allocation (EIO for every frame)
 		size_t fr = 0, tot = 0;
 		if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr) {
-			const uint64_t cap = (uint64_t)fr / 8192u;  // = fr * 3/8 / (2 slots x 1.5 KB)
+			const uint64_t cap = (uint64_t)fr / 16384u;  // = fr * 3/8 / (4 slots x 1.5 KB)
 			const uint64_t floor_mbs = 1u << 15;         // one 4K frame and change
 			if (cap < chunk_mbs_tok) chunk_mbs_tok = cap > floor_mbs ? cap : floor_mbs;
 			if (cap < chunk_mbs_pk) chunk_mbs_pk = cap > floor_mbs ? cap : floor_mbs;
@@ -422,8 +460,8 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 	uint32_t released = 0;  // positions whose frames' host data is freed (all below this one)
 	const char* where = nullptr;
 	hipError_t he = hipSuccess;
-	// The host frames of the last chunks are released by a detached thread once the call has its
-	// results: freeing them is when glibc trims the heap those frames grew (GBs of packed data,
+	// The host frames of the last chunks are released by the background freer (g_freer) once the
+	// call has its results: freeing them is when glibc trims the heap those frames grew (GBs of packed data,
 	// ~0.3 s at 1024 4K frames), work the caller need not wait for.
 	bool defer_release = false;
 	std::vector<Vp8gPackedFrame> late;
@@ -520,10 +558,14 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 			}
 			const uint32_t nf = (uint32_t)idx.size();
 			// -- launch geometry (the choices vp8g_reconstruct_batch makes)
+			// Split mode (a frame over several co-resident workgroups that spin on each other) only
+			// for a chunk that is the call's only one: chunks on the other slots' streams -- a long
+			// device-m05 kernel, the other host slot -- could hold the CUs a part is waiting for.
+			const bool alone = a == 0 && b == n;
 			uint32_t nw = vp8g::pick_waves(0, max_rows, nf);
-			if (vp8g::pick_split(0, nf, 8, max_rows) > 1) nw = 8;
+			if (alone && vp8g::pick_split(0, nf, 8, max_rows) > 1) nw = 8;
 			const bool big = vp8g::lds_bytes((int)nw, max_cols, false) > (size_t)vp8g::kMaxLds;
-			const uint32_t k = big ? 1u : vp8g::pick_split(0, nf, nw, max_rows);
+			const uint32_t k = big || !alone ? 1u : vp8g::pick_split(0, nf, nw, max_rows);
 			ChunkLayout L;
 			uint64_t o = 0;
 			L.ym = o, o = al256(o + mbs);
@@ -680,9 +722,7 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 	for (Copier& c : copiers) (void)hipStreamDestroy(c.stream);
 	if (trace) fprintf(stderr, "[pipe] buffers freed at %.1f ms\n", ms_now());
 	if (!late.empty()) {  // (started last: its heap trimming would contend with the device-memory frees above)
-		std::thread([v = std::move(late)]() mutable {
-			for (Vp8gPackedFrame& p : v) vp8f_packed_free(&p);
-		}).detach();
+		g_freer.post(std::move(late));
 	}
 	{
 		int first = 0;

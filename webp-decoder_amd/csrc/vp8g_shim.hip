@@ -320,6 +320,11 @@ VP8G_API int vp8g_decode_batch_device(const Vp8gFrameDesc* h_descs, const Vp8gFr
 		errno = EINVAL;
 		return -1;
 	}
+	for (uint32_t i = 0; i < n; i++)  // (all-zero descriptors are allowed: empty slots, no work)
+		if (h_descs[i].mb_cols > 1024 || h_descs[i].mb_rows > 1024 || (!h_descs[i].mb_cols != !h_descs[i].mb_rows)) {
+			errno = EINVAL;
+			return -1;
+		}
 	std::vector<Vp8gFrameDesc> v(h_descs, h_descs + n);
 	std::lock_guard<std::mutex> lk(g_dev.mu);
 	return run_locked(v, *arrays, d_out, (hipStream_t)stream, waves, (uint8_t*)d_descs, false);
