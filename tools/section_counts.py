@@ -18,7 +18,8 @@ subprocess.check_call(cmd)
 lines = open(out).read().split("\n")
 sym = None
 for l in lines:
-    m = re.match(r"^(_ZN\S*frame_kernelILi%sELb0E\S*):\s*(;.*)?$" % nw, l)
+    # NW, or a mangled template-argument fragment such as 16ELb0ELb0ELb1 (the chain kernel)
+    m = re.match(r"^(_ZN\S*frame_kernelILi%s\S*):\s*(;.*)?$" % (nw if "E" in nw else nw + "ELb0ELb0ELb0"), l)
     if m:
         sym = m.group(1)
         break
@@ -30,6 +31,7 @@ body = lines[start:end]
 sec = "pre"
 counts = collections.OrderedDict()
 def cls(op):
+    if op.startswith("v_readlane") or op.startswith("v_writelane"): return "spill"
     if op.startswith("v_") : return "valu"
     if op.startswith("s_cbranch") or op.startswith("s_branch"): return "branch"
     if op.startswith("s_waitcnt") or op.startswith("s_sleep") or op.startswith("s_nop"): return "wait"
@@ -47,8 +49,8 @@ for l in body:
         continue
     op = t.split()[0]
     counts.setdefault(sec, collections.Counter())[cls(op)] += 1
-names = {"pre": "setup/prefetch+residual", "after_0": "wait", "after_1": "borders", "after_2": "predict+bpred",
+names = {"pre": "prologue/pair setup", "after_30": "side info+residual+prefetch", "after_0": "wait", "after_1": "borders", "after_2": "predict+bpred",
          "after_3": "save ctx", "after_4": "loop filter", "after_5": "flush", "after_6": "publish/loop"}
-print("%-26s %6s %6s %6s %6s %6s %6s" % ("section", "valu", "salu", "branch", "lds", "vmem", "wait"))
+print("%-26s %6s %6s %6s %6s %6s %6s %6s" % ("section", "valu", "salu", "branch", "lds", "vmem", "wait", "lanes"))
 for k, c in counts.items():
-    print("%-26s %6d %6d %6d %6d %6d %6d" % (names.get(k, k), c["valu"], c["salu"], c["branch"], c["lds"], c["vmem"], c["wait"]))
+    print("%-26s %6d %6d %6d %6d %6d %6d %6d" % (names.get(k, k), c["valu"], c["salu"], c["branch"], c["lds"], c["vmem"], c["wait"], c["spill"]))

@@ -48,7 +48,9 @@ constexpr int kBpTable = 64;      // B_PRED predictor table: 11 modes x 16 px x 
 constexpr int kBpModes = 11;      // modes 0..9 + one constant-128 entry for out-of-range modes
 constexpr int kDqTable = kBpTable + kBpModes * 16 * 16;  // 4 segments x 6 int16 dequant factors
 constexpr int kLfTable = kDqTable + 48;                 // 4 segments x 2 (B_PRED?) x {E, I, T, 0}
-constexpr int kHdrBytes = kLfTable + 32;
+constexpr int kTabStride = 80;                          // per frame slot (chain mode: two slots)
+constexpr int kMisc = kDqTable + 2 * kTabStride;        // chain mode: list length
+constexpr int kHdrBytes = kMisc + 16;
 
 // Shared per-MB-column context (one frame per workgroup).
 constexpr int kCtxRecBytes = 32;   // unfiltered bottom row: Y 16, U 8, V 8 (intra prediction)
@@ -83,6 +85,12 @@ __host__ __device__ inline uint32_t cost_class(const Vp8gFrameDesc& d) {
 inline size_t lds_bytes(int waves, uint32_t ctx_cols, bool global_ctx) {
 	return (size_t)kHdrBytes + (size_t)waves * kWaveBytes + (global_ctx ? 0 : (size_t)ctx_cols * kCtxBytesPerCol);
 }
+// Chain mode (one 16-wave workgroup per CU decoding a list of frames, vp8g_kernels.hip): two
+// context slots and the list (at most list_max frames).
+constexpr int kChainWaves = 16;
+inline size_t chain_lds_bytes(uint32_t ctx_cols, uint32_t list_max) {
+	return (size_t)kHdrBytes + (size_t)kChainWaves * kWaveBytes + 2 * (size_t)ctx_cols * kCtxBytesPerCol + 4 * (size_t)list_max;
+}
 
 // Launch the fused recon(+LF) kernel.  `global_ctx` != nullptr selects the variant whose
 // per-column context lives in device memory (frames too wide for LDS); it must hold
@@ -101,6 +109,13 @@ hipError_t launch_frames(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const 
 // pick_order returns F = the CU count when that is worth it (classes differ, more frames than
 // CUs), else 0.
 uint32_t pick_order(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint32_t nsplit);
+
+// Chain mode for n_frames frames on this device: the workgroup count (0 = not applicable: too few
+// frames, a context too wide for two LDS slots, or VP8G_CHAIN=0), and whether the frames are
+// placed by cost class (*ordered; needs the sort scratch to fit the context slots).
+uint32_t pick_chain(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint32_t ctx_cols, bool* ordered);
+hipError_t launch_chain(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const Vp8gBatchArrays& arrays, uint8_t* d_out,
+                        uint32_t ctx_cols, hipStream_t stream, uint32_t workgroups, bool ordered);
 
 constexpr uint32_t kMaxSplit = 8;
 int device_cus();

@@ -582,48 +582,140 @@ DEV uint32_t ordered_frame(const Vp8gFrameDesc* descs, uint32_t n, uint32_t F, u
 	return f;
 }
 
-template <int NW, bool kG, bool kS>
+// Chain mode (kC, batches with more frames than CUs): ONE workgroup of NW = 16 waves per CU
+// decodes a list of frames as one continuous chain of MB row pairs -- global pair g of the list
+// (the frames' pairs one after another) belongs to wave g % NW -- so no wave idles at a frame's
+// end while another frame of the CU still has rows, and a heavy frame never runs alone on half
+// the CU.  Two frames are in flight at once: frame j of the list uses LDS slot j & 1 (its
+// per-column context and its dequant / loop-filter tables); pair 0 of frame j waits until frame
+// j - 2, the slot's previous user, has finished its last pair (which implies all of its pairs:
+// pair k's last steps wait for pair k - 1 to complete).  The list of workgroup b: the frames at
+// positions b, 2W-1-b, 2W+b, 4W-1-b, ... of the batch sorted by descending cost class (snake
+// order: every CU gets one of the heaviest and one of the lightest frames per two rounds), sorted
+// in the prologue by wave 0 (stable counting sort over the cost classes in LDS scratch).
+// Progress words encode global pair * 2048 + steps done (C <= 1024, so steps <= 1026).
+constexpr uint32_t kProgShift = 11;
+
+template <int NW, bool kG, bool kS, bool kC>
 __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kernel(const Vp8gFrameDesc* __restrict__ descs, Vp8gBatchArrays A,
                                                         uint8_t* __restrict__ out, uint32_t ctx_cols,
                                                         uint8_t* __restrict__ gctx, uint32_t nsplit,
                                                         uint8_t* __restrict__ mbox, uint32_t* __restrict__ gprog,
-                                                        uint32_t ord_first) {
+                                                        uint32_t ord_first, uint32_t n_chain) {
+	static_assert(!kC || (!kG && !kS), "chain mode keeps the context in LDS and never splits");
 	extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 	const int lane0 = (int)(threadIdx.x & 63);
 	const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
 	const uint32_t K = kS ? nsplit : 1u;
 	const uint32_t nfr = kS ? gridDim.x / K : gridDim.x;
-	const uint32_t f = kS ? blockIdx.x % nfr : (ord_first ? ordered_frame<NW * 64>(descs, nfr, ord_first, smem) : blockIdx.x);
+	const uint32_t slot_bytes = ctx_cols * (uint32_t)kCtxBytesPerCol;
+	uint8_t* const ctx_base = smem + kHdrBytes + NW * kWaveBytes;
+	uint32_t* const chain_list = (uint32_t*)(ctx_base + 2 * slot_bytes);  // (kC) after the two context slots
+	uint32_t m_chain = 1;  // (kC) frames in this workgroup's list
+	uint32_t f;
+	if constexpr (kC) {
+		// ---- this workgroup's frame list (see above); ord_first != 0: cost-sorted positions
+		const uint32_t Wg = gridDim.x, b = blockIdx.x, n = n_chain;
+		if (wave == 0) {
+			uint32_t* const hist = (uint32_t*)ctx_base;  // scratch (the context slots, written later)
+			uint32_t* const sorted = hist + kCostClasses;
+			const uint64_t lt = (1ull << lane0) - 1ull;
+			if (ord_first) {
+				for (int i = lane0; i < (int)kCostClasses; i += 64) hist[i] = 0u;
+				wave_lds_sync();
+				for (int pass = 0; pass < 2; pass++) {
+					for (uint32_t c0 = 0; c0 < n; c0 += 64) {
+						const uint32_t i = c0 + (uint32_t)lane0;
+						const bool valid = i < n;
+						const uint32_t cls = valid ? cost_class(descs[i]) : 0u;
+						uint64_t rem = __ballot(valid);
+						while (rem) {  // one distinct class per iteration (peeled by its first lane)
+							const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cls, (int)__builtin_ctzll(rem));
+							const uint64_t mk = __ballot(valid && cls == c);
+							const uint32_t base = hist[c];
+							wave_lds_sync();
+							if (pass == 1 && ((mk >> lane0) & 1ull)) sorted[base + (uint32_t)__popcll(mk & lt)] = i;
+							if (lane0 == (int)__builtin_ctzll(mk)) hist[c] = base + (uint32_t)__popcll(mk);
+							wave_lds_sync();
+							rem &= ~mk;
+						}
+					}
+					if (pass == 0) {  // counts -> start positions, heaviest class first
+						if (lane0 == 0) {
+							uint32_t acc = 0;
+							for (int c = (int)kCostClasses - 1; c >= 0; c--) {
+								const uint32_t h = hist[c];
+								hist[c] = acc;
+								acc += h;
+							}
+						}
+						wave_lds_sync();
+					}
+				}
+			}
+			// snake positions of workgroup b (increasing in j), empty descriptors left out
+			uint32_t cnt = 0;
+			for (uint32_t j0 = 0;; j0 += 64) {
+				const uint32_t j = j0 + (uint32_t)lane0;
+				const uint32_t pos = j * Wg + ((j & 1u) ? Wg - 1u - b : b);
+				const bool valid = pos < n;
+				if (__ballot(valid) == 0ull) break;
+				const uint32_t fi = valid ? (ord_first ? sorted[pos] : pos) : 0u;
+				const bool keep = valid && descs[fi].mb_cols != 0 && descs[fi].mb_rows != 0;
+				const uint64_t mk = __ballot(keep);
+				if (keep) chain_list[cnt + (uint32_t)__popcll(mk & lt)] = fi;
+				cnt += (uint32_t)__popcll(mk);
+			}
+			if (lane0 == 0) *(uint32_t*)(smem + kMisc) = cnt;
+		}
+		__syncthreads();
+		m_chain = (uint32_t)__builtin_amdgcn_readfirstlane((int)*(const uint32_t*)(smem + kMisc));
+		f = m_chain ? (uint32_t)__builtin_amdgcn_readfirstlane((int)chain_list[0]) : 0u;
+	} else {
+		f = kS ? blockIdx.x % nfr : (ord_first ? ordered_frame<NW * 64>(descs, nfr, ord_first, smem) : blockIdx.x);
+	}
 	const uint32_t part = kS ? blockIdx.x / nfr : 0u;
-	const Vp8gFrameDesc& D = descs[f];
 
 	for (int i = (int)threadIdx.x; i < kBpModes * 64; i += NW * 64) ((uint32_t*)(smem + kBpTable))[i] = kBpTab.v[i];
 	uint32_t bt_l = kBorderTab.v[lane0 & 31];  // this lane's border-setup role (loop-invariant)
-	if (threadIdx.x < 24) ((int16_t*)(smem + kDqTable))[threadIdx.x] = D.dq[threadIdx.x / 6][threadIdx.x % 6];
-	if (threadIdx.x < 32) smem[kLfTable + threadIdx.x] = D.lf[threadIdx.x >> 3][(threadIdx.x >> 2) & 1][threadIdx.x & 3];
+	// dequant / loop-filter tables of a frame into its slot (chain mode: by the wave of the frame's pair 0)
+	auto put_tables = [&](const Vp8gFrameDesc& Df, uint32_t tabo, int l) {
+		if (l < 24) ((int16_t*)(smem + kDqTable + tabo))[l] = Df.dq[l / 6][l % 6];
+		if (l < 32) smem[kLfTable + tabo + l] = Df.lf[l >> 3][(l >> 2) & 1][l & 3];
+	};
+	if constexpr (!kC) put_tables(descs[f], 0u, (int)threadIdx.x);
 	if (threadIdx.x < 16) ((uint32_t*)(smem + kProgress))[threadIdx.x] = 0;
 	__syncthreads();
+	if (kC && m_chain == 0) return;
 
-	const uint32_t C = D.mb_cols, R = D.mb_rows;
-	const uint32_t flags = D.flags;
-	uint32_t flags_l = flags;  // (laundered per step, VP8G_LAUNDER)
-	[[maybe_unused]] const bool lf_on = (flags & VP8G_F_LOOPFILTER) != 0;
-	[[maybe_unused]] const bool simple = (flags & VP8G_F_SIMPLE) != 0;
-	const bool lf_only = (flags & VP8G_F_LF_ONLY) != 0;
-	const uint64_t mb0 = D.mb_offset;
-	uint8_t* const outY = out + D.out_y;
-	uint8_t* const outU = out + D.out_u;
-	const uint32_t W = D.width, H = D.height, CW = (D.width + 1) >> 1, CH = (D.height + 1) >> 1;
-	const uint32_t sy = D.stride_y, suv = D.stride_uv;
-	const uint32_t vofs = (uint32_t)(D.out_v - D.out_u);  // V plane relative to U (< 2^32 by construction)
-	const uint32_t yal = (uint32_t)(uintptr_t)outY, ual = (uint32_t)(uintptr_t)outU;  // alignment tests
-	const Rsrc rY = plane_rsrc(outY, sy * H), rC = plane_rsrc(outU, vofs + suv * CH);  // output planes
-	uint32_t* const prog = (uint32_t*)(smem + kProgress);
+	// ---- the current frame (chain mode: reloaded when the wave's next pair is in another frame)
+	const Vp8gFrameDesc* Dp;
+	uint32_t C, R, flags, W, H, CW, CH, sy, suv, vofs, yal, ual, npairs, CP2, tabo;
+	uint64_t mb0;
+	uint8_t* outY;
+	uint8_t* outU;
 	Ctx<kG> ctx;
-	ctx.lds = smem + kHdrBytes + NW * kWaveBytes;
-	ctx.g = kG ? gctx + (size_t)f * ctx_cols * kCtxBytesPerCol : nullptr;
-	const uint32_t npairs = (R + 1) >> 1;
-	const uint32_t CP2 = C + 2;
+	auto set_frame = [&](uint32_t fi, uint32_t slot) {
+		Dp = descs + fi;
+		const Vp8gFrameDesc& D = *Dp;
+		C = D.mb_cols, R = D.mb_rows;
+		flags = D.flags;
+		mb0 = D.mb_offset;
+		outY = out + D.out_y;
+		outU = out + D.out_u;
+		W = D.width, H = D.height, CW = (D.width + 1) >> 1, CH = (D.height + 1) >> 1;
+		sy = D.stride_y, suv = D.stride_uv;
+		vofs = (uint32_t)(D.out_v - D.out_u);  // V plane relative to U (< 2^32 by construction)
+		yal = (uint32_t)(uintptr_t)outY, ual = (uint32_t)(uintptr_t)outU;  // alignment tests
+		ctx.lds = ctx_base + slot * slot_bytes;
+		ctx.g = kG ? gctx + (size_t)fi * ctx_cols * kCtxBytesPerCol : nullptr;
+		npairs = (R + 1) >> 1;
+		CP2 = C + 2;
+		tabo = slot * (uint32_t)kTabStride;
+	};
+	set_frame(f, 0u);
+	uint32_t flags_l = flags;  // (laundered per step, VP8G_LAUNDER)
+	uint32_t* const prog = (uint32_t*)(smem + kProgress);
 	const uint32_t GW = K * NW, gw = part * NW + (uint32_t)wave;
 	const size_t chan = (size_t)ctx_cols * kCtxBytesPerCol;
 	const uint32_t pin = (part + K - 1) % K;  // the part holding this part's wave-0 predecessors
@@ -635,7 +727,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 #ifdef VP8G_STAMPS
 	uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 	uint64_t st_prev = __builtin_amdgcn_s_memtime();
-	if (f == 0 && lane0 == 0 && wave < 32) g_vp8g_wave_times[2 * wave] = __builtin_amdgcn_s_memrealtime();
+	if (blockIdx.x == 0 && lane0 == 0 && wave < 32) g_vp8g_wave_times[2 * wave] = __builtin_amdgcn_s_memrealtime();
 	const uint64_t st_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
 
@@ -661,13 +753,67 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 	// Set once a dependency wait has timed out: the wave finishes without waiting again (its output
 	// is garbage and the status word says so), so a stalled producer costs one bound, not one per step.
 	bool dead = false;
-	for (uint32_t k = gw; k < npairs; k += GW) {
+	// bounded wait until the progress word of wave pw reaches `need`
+	auto wait_prog = [&](uint32_t pw, uint32_t need, bool xin_) {
+		uint32_t spins = 0;
+		uint64_t t0 = 0;
+		while (((kS && xin_) ? __hip_atomic_load(gp_in, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+		             : __hip_atomic_load(prog + pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < need) {
+			__builtin_amdgcn_s_sleep(1);
+			if ((++spins & 1023u) == 0) {
+				const uint64_t now = __builtin_amdgcn_s_memrealtime();
+				if (t0 == 0) t0 = now;
+				else if (now - t0 > (uint64_t)VP8G_WAIT_TICKS) {  // give up, flag it, and never wait again
+					if (lane0 == 0) atomicOr(A.status, VP8G_ERR_TIMEOUT);
+					dead = true;
+					break;
+				}
+			}
+		}
+		asm volatile("" ::: "memory");
+	};
+	// chain mode: list index of the wave's current frame, its first global pair, and the last global
+	// pair (with its step count) of the frames one and two list positions back
+	uint32_t jf = 0, gbase = 0, last1 = ~0u, T1 = 0, last2 = ~0u, T2 = 0;
+	for (uint32_t g = gw;; g += GW) {
+		uint32_t k;
+		if constexpr (kC) {
+			while (g >= gbase + npairs) {  // advance to the frame holding global pair g
+				last2 = last1, T2 = T1;
+				last1 = gbase + npairs - 1u, T1 = 2u * npairs - 1u < R ? CP2 : C;
+				gbase += npairs;
+				if (++jf >= m_chain) break;
+				set_frame((uint32_t)__builtin_amdgcn_readfirstlane((int)chain_list[jf]), jf & 1u);
+			}
+			if (jf >= m_chain) break;
+			k = g - gbase;
+			if (k == 0) {
+				// claim slot jf & 1: frame jf - 2 must be done with it, then this frame's tables
+				if (last2 != ~0u && !dead) wait_prog(last2 % NW, (last2 << kProgShift) + T2, false);
+				put_tables(*Dp, tabo, lane0);
+				wave_lds_sync();
+			} else if (!dead) {
+				// step 0's dependency wait, before its residual: the residual reads the dequant table
+				// that pair 0 writes when it claims the slot (pair k - 1 past step 0 implies pair 0 past
+				// it, and pair 0 writes its tables before its first publish)
+				wait_prog((uint32_t)((wave + NW - 1) % NW), ((g - 1u) << kProgShift) + 1u, false);
+			}
+		} else {
+			k = g;
+			if (k >= npairs) break;
+		}
+		// output planes (built per pair: a buffer resource carried around the chain's frame loop
+		// would be a loop PHI the backend cannot keep in SGPRs)
+		const Rsrc rY = plane_rsrc(outY, sy * H), rC = plane_rsrc(outU, vofs + suv * CH);
 		const bool xin = kS && wave == 0 && k > 0;             // predecessor pair in another part
 		const bool xout = kS && wave == NW - 1 && k + 1 < npairs;  // successor pair in another part
 		u32x4 mbx = u32x4{0u, 0u, 0u, 0u};                     // mailbox prefetch (xin: lanes 0..9)
 		const uint32_t rA = 2 * k;
 		const bool two = rA + 1 < R;
 		const uint32_t T = two ? CP2 : C;
+		[[maybe_unused]] const bool lf_on = (flags & VP8G_F_LOOPFILTER) != 0;
+		[[maybe_unused]] const bool simple = (flags & VP8G_F_SIMPLE) != 0;
+		const bool lf_only = (flags & VP8G_F_LF_ONLY) != 0;
 		// Per-lane row bases of this pair (lane roles: ln 0..24 one 32-B coefficient block each --
 		// Y 0..15, U 16..19, V 20..23, Y2 24 (and 26..31, duplicates) -- ln 25 the 16 B_PRED modes;
 		// side bytes ln&3: ymode, uv_mode, segment_id, has_coeff for lanes 26..29).  MB m's data
@@ -717,6 +863,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 		// prefetched data waits for the loads alone, never for stores (see kNoStore)
 		bst128(rY, kNoStore, u32x4{0u, 0u, 0u, 0u});
 		bst64(rC, kNoStore, u32x2{0u, 0u});
+		flags_l = (uint32_t)__builtin_amdgcn_readfirstlane((int)flags);  // (the chain's frame loop makes it a PHI)
 
 		for (uint32_t t = 0; t < T; t++) {
 			// Lane-derived values are recomputed every step from a laundered lane id: hoisting the
@@ -763,6 +910,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			                        (uint32_t)__builtin_amdgcn_ds_bpermute(bml, (int)cur.a.w)};
 
 			// ---------------------------------------------- residual (no spatial dependency)
+			SUBMARK(30);
 			PRIO(0);
 			// Computed before the dependency wait.  Each block stays in its lane's registers (rs[],
 			// packed int16 pairs) for the whole-block predictors of the same lane; the luma blocks
@@ -776,7 +924,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 				// vertical pass wrap mod 2^16 exactly like the reference's int16 stores; the
 				// horizontal pass (whose (x + 4) >> 3 needs the full-precision sum) runs in 32 bits.
 				const int cls = ln < 16 ? 0 : (ln < 24 ? 1 : 2);  // Y1, UV, Y2 factors
-				const uint32_t* dqt = (const uint32_t*)(smem + kDqTable) + seg * 3 + cls;
+				const uint32_t* dqt = (const uint32_t*)(smem + kDqTable + tabo) + seg * 3 + cls;
 				const uint32_t fdcac = *dqt;  // (dc, ac) int16 pair
 				const uint32_t facac = __builtin_amdgcn_perm(fdcac, fdcac, 0x03020302u);
 				uint32_t w[8] = {pk_mul(cur.a.x, fdcac), pk_mul(cur.a.y, facac), pk_mul(cur.a.z, facac), pk_mul(cur.a.w, facac),
@@ -856,24 +1004,9 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			if (k > 0 && !dead && !(VP8G_ABLATE & 8)) {
 				// (one column more lag across parts: the mailbox is read a step ahead of use)
 				const uint32_t lag = xin ? 5u : 4u;
-				const uint32_t need = (k - 1) * CP2 + ((t + lag < CP2) ? t + lag : CP2);
-				const uint32_t pw = (uint32_t)((wave + NW - 1) % NW);
-				uint32_t spins = 0;
-				uint64_t t0 = 0;
-				while ((xin ? __hip_atomic_load(gp_in, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-				            : __hip_atomic_load(prog + pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < need) {
-					__builtin_amdgcn_s_sleep(1);
-					if ((++spins & 1023u) == 0) {
-						const uint64_t now = __builtin_amdgcn_s_memrealtime();
-						if (t0 == 0) t0 = now;
-						else if (now - t0 > (uint64_t)VP8G_WAIT_TICKS) {  // give up, flag it, and never wait again
-							if (lane == 0) atomicOr(A.status, VP8G_ERR_TIMEOUT);
-							dead = true;
-							break;
-						}
-					}
-				}
-				asm volatile("" ::: "memory");
+				const uint32_t ahead = (t + lag < CP2) ? t + lag : CP2;
+				if (xin) wait_prog(0u, (k - 1) * CP2 + ahead, true);
+				else wait_prog((uint32_t)((wave + NW - 1) % NW), ((g - 1u) << kProgShift) + ahead, false);
 			}
 			if (kS && xin) {
 				// mailbox -> this part's LDS ctx: rec[t + 1] and lf[t] now (loaded last step; at t = 0
@@ -909,13 +1042,13 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					// loop-filter-only mode: the MB's pixels come from the padded input image
 					const uint8_t* src = A.src;
 					if (ln < 16) {
-						const uint8_t* s = src + D.src_y + (size_t)(y0 + ln) * D.src_stride_y + x0;
+						const uint8_t* s = src + Dp->src_y + (size_t)(y0 + ln) * Dp->src_stride_y + x0;
 						uint8_t* const td = tY + (4 + ln) * kTP + slot * 16;
 						st64(td, u32x2{ld32(s), ld32(s + 4)});
 						st64(td + 8, u32x2{ld32(s + 8), ld32(s + 12)});
 					} else {
 						const int p = (ln - 16) >> 3, row = ln & 7;
-						const uint8_t* s = src + (p ? D.src_v : D.src_u) + (size_t)(cy0 + row) * D.src_stride_uv + cx0;
+						const uint8_t* s = src + (p ? Dp->src_v : Dp->src_u) + (size_t)(cy0 + row) * Dp->src_stride_uv + cx0;
 						stc64(tC + p * kCV + (4 + row) * kTP + slot * 8, u32x2{ld32(s), ld32(s + 4)});
 					}
 				} else {
@@ -1090,7 +1223,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			// ---------------------------------------------- loop filter MB(r, c)
 			PRIO(5);
 			if (lf_on && !(VP8G_ABLATE & 1)) {
-				const uint8_t* lp = smem + kLfTable + seg * 8 + (bpred ? 4 : 0);
+				const uint8_t* lp = smem + kLfTable + tabo + seg * 8 + (bpred ? 4 : 0);
 				const int E = lp[0], I = lp[1], Tt = lp[2];
 				const bool en = act && E != 0;
 				if (__ballot(en) != 0ull) {
@@ -1263,7 +1396,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 				if (lane == 0) __hip_atomic_store(gp_out, k * CP2 + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 			}
 			if (lane == 0 && wave != VP8G_TEST_STALL_WAVE)
-				__hip_atomic_store(prog + wave, k * CP2 + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+				__hip_atomic_store(prog + wave, (g << kProgShift) + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 			STAMP(7);
 		}
 	}
@@ -1290,13 +1423,13 @@ hipError_t launch_t(const Vp8gFrameDesc* d_descs, uint32_t n, const Vp8gBatchArr
                     uint32_t ctx_cols, uint8_t* gctx, uint32_t nsplit, uint8_t* mbox, uint32_t* gprog, hipStream_t stream,
                     uint32_t ord_first = 0) {
 	const size_t lds = lds_bytes(NW, ctx_cols, kG);
-	auto fn = frame_kernel<NW, kG, kS>;
+	auto fn = frame_kernel<NW, kG, kS, false>;
 	if (lds > 65536) {
 		hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
 		if (e != hipSuccess) return e;
 	}
 	hipLaunchKernelGGL(fn, dim3(n * (kS ? nsplit : 1u)), dim3(NW * 64), lds, stream, d_descs, arrays, d_out, ctx_cols, gctx,
-	                   nsplit, mbox, gprog, kS ? 0u : ord_first);
+	                   nsplit, mbox, gprog, kS ? 0u : ord_first, 0u);
 	return hipGetLastError();
 }
 
@@ -1375,6 +1508,41 @@ uint32_t pick_order(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint32_t ns
 	for (uint32_t i = 1; i < n_frames; i++)
 		if (cost_class(h_descs[i]) != c0) return (uint32_t)n_cus;
 	return 0;  // uniform batch: the order would be the identity
+}
+
+uint32_t pick_chain(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint32_t ctx_cols, bool* ordered) {
+#ifndef VP8G_CHAIN_DEFAULT  // (A/B builds: -DVP8G_CHAIN_DEFAULT=0)
+#define VP8G_CHAIN_DEFAULT 0  // (off until validated on the GPU)
+#endif
+	static const int mode = [] {  // VP8G_CHAIN=0: never (A/B experiments), =1: also for batches <= the CU count
+		const char* e = getenv("VP8G_CHAIN");
+		return e ? atoi(e) : VP8G_CHAIN_DEFAULT;
+	}();
+	*ordered = false;
+	const int n_cus = device_cus();
+	if (mode == 0 || n_cus <= 0 || n_frames == 0 || (mode < 0 && n_frames <= (uint32_t)n_cus)) return 0;
+	const uint32_t wg = n_frames < (uint32_t)n_cus ? n_frames : (uint32_t)n_cus;
+	const uint32_t list_max = (n_frames + wg - 1) / wg;
+	if (ctx_cols > 1024 || chain_lds_bytes(ctx_cols, list_max) > (size_t)kMaxLds) return 0;
+	// cost-class placement when the classes differ and the sort scratch fits the context slots
+	const uint32_t c0 = cost_class(h_descs[0]);
+	bool differ = false;
+	for (uint32_t i = 1; i < n_frames && !differ; i++) differ = cost_class(h_descs[i]) != c0;
+	*ordered = differ && (size_t)4 * (kCostClasses + n_frames) <= 2 * (size_t)ctx_cols * kCtxBytesPerCol && pick_order(h_descs, n_frames, 1) != 0;
+	return wg;
+}
+
+hipError_t launch_chain(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const Vp8gBatchArrays& arrays, uint8_t* d_out,
+                        uint32_t ctx_cols, hipStream_t stream, uint32_t workgroups, bool ordered) {
+	if (n_frames == 0) return hipSuccess;
+	const uint32_t list_max = (n_frames + workgroups - 1) / workgroups;
+	const size_t lds = chain_lds_bytes(ctx_cols, list_max);
+	auto fn = frame_kernel<kChainWaves, false, false, true>;
+	hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+	if (e != hipSuccess) return e;
+	hipLaunchKernelGGL(fn, dim3(workgroups), dim3(kChainWaves * 64), lds, stream, d_descs, arrays, d_out, ctx_cols, nullptr, 1u,
+	                   nullptr, nullptr, ordered ? 1u : 0u, n_frames);
+	return hipGetLastError();
 }
 
 hipError_t launch_frames(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const Vp8gBatchArrays& arrays,

@@ -679,10 +679,16 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 					                   (int16_t*)(d + L.cv), (int16_t*)(d + L.cy2));
 					PTRY(hipGetLastError(), "expand launch");
 				}
-				PTRY(vp8g::launch_frames((const Vp8gFrameDesc*)(d + L.desc), nf, arr, d + L.out, max_cols, max_rows,
-				                         big ? d + L.gctx : nullptr, stream, nw, k, k > 1 ? d + L.mbox : nullptr,
-				                         k > 1 ? (uint32_t*)(d + L.gprog) : nullptr),
-				     "recon launch");
+				bool ordered = false;
+				const uint32_t wg = big || k > 1 ? 0u : vp8g::pick_chain(s.descs.data(), nf, max_cols, &ordered);
+				if (wg)  // more frames than CUs: one 16-wave chain of frames per CU
+					PTRY(vp8g::launch_chain((const Vp8gFrameDesc*)(d + L.desc), nf, arr, d + L.out, max_cols, stream, wg, ordered),
+					     "recon launch");
+				else
+					PTRY(vp8g::launch_frames((const Vp8gFrameDesc*)(d + L.desc), nf, arr, d + L.out, max_cols, max_rows,
+					                         big ? d + L.gctx : nullptr, stream, nw, k, k > 1 ? d + L.mbox : nullptr,
+					                         k > 1 ? (uint32_t*)(d + L.gprog) : nullptr),
+					     "recon launch");
 			}
 			// -- D2H into the callers' images, by this kind's Copier once the kernels are done
 			PTRY(hipEventRecord(s.kdone, stream), "event");

@@ -220,6 +220,14 @@ int run_locked(const std::vector<Vp8gFrameDesc>& descs, const Vp8gBatchArrays& a
 		gprog = (uint32_t*)(g_dev.mbox + mb);
 		HIP_TRY(hipMemsetAsync(gprog, 0, pb, s), "memset(progress)");
 	}
+	if (!big && k == 1 && !waves_hint) {  // more frames than CUs: one 16-wave chain of frames per CU
+		bool ordered = false;
+		const uint32_t wg = vp8g::pick_chain(descs.data(), n, max_cols, &ordered);
+		if (wg) {
+			HIP_TRY(vp8g::launch_chain((const Vp8gFrameDesc*)d_descs, n, arr, d_out, max_cols, s, wg, ordered), "launch");
+			return 0;
+		}
+	}
 	const uint32_t ord = vp8g::pick_order(descs.data(), n, k);  // cost-balanced placement (vp8g_device.h)
 	HIP_TRY(vp8g::launch_frames((const Vp8gFrameDesc*)d_descs, n, arr, d_out, max_cols, max_rows, gctx, s, nw, k, mbox, gprog, ord),
 	        "launch");
