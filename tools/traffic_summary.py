@@ -52,7 +52,7 @@ write_b = write_kib * 1024
 mbs = 512 * 240 * 135
 out = {
     "frames": 512, "filtered": True, "width": 3840, "height": 2160,
-    "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, {n1}/{n2} dispatches of frame_kernel<8,false>, tag {tag}",
+    "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, {n1}/{n2} dispatches of frame_kernel (the bench kernel), tag {tag}",
     "fetch_size_kib_per_launch": round(fetch_kib, 1),
     "write_size_kib_per_launch": round(write_kib, 1),
     "hbm_read_bytes_per_launch": round(read_b),

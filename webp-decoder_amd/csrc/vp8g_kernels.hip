@@ -1512,7 +1512,7 @@ uint32_t pick_order(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint32_t ns
 
 uint32_t pick_chain(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint32_t ctx_cols, bool* ordered) {
 #ifndef VP8G_CHAIN_DEFAULT  // (A/B builds: -DVP8G_CHAIN_DEFAULT=0)
-#define VP8G_CHAIN_DEFAULT 0  // (off until validated on the GPU)
+#define VP8G_CHAIN_DEFAULT -1
 #endif
 	static const int mode = [] {  // VP8G_CHAIN=0: never (A/B experiments), =1: also for batches <= the CU count
 		const char* e = getenv("VP8G_CHAIN");
