@@ -76,6 +76,19 @@ OPS = [
     ("v_cvt_f32_i32", "v_cvt_f32_i32 {r}, {r}"),
     ("v_floor_f32", "v_floor_f32 {r}, {r}"),
     ("v_min3_i32", "v_min3_i32 {r}, {r}, {k}, {r}"),
+    # third pass (r03g): saturating packs, 16-bit forms, bitop3, lane swaps
+    ("v_sat_pk_u8_i16", "v_sat_pk_u8_i16 {r}, {r}"),
+    ("v_med3_i16", "v_med3_i16 {r}, {r}, {k}, {r}"),
+    ("v_max_i16", "v_max_i16 {r}, {r}, {k}"),
+    ("v_sub_i16_clamp", "v_sub_i16 {r}, {r}, {k} clamp"),
+    ("v_add_u16_clamp", "v_add_u16 {r}, {r}, {k} clamp"),
+    ("v_pk_add_i16_clamp", "v_pk_add_i16 {r}, {r}, {k} clamp"),
+    ("v_bitop3_b32", "v_bitop3_b32 {r}, {r}, {k}, {r} bitop3:0xca"),
+    ("v_permlane32_swap", "v_permlane32_swap_b32 {r}, {k}"),
+    ("v_lshlrev_b16", "v_lshlrev_b16 {r}, 1, {r}"),
+    ("v_mul_lo_u32", "v_mul_lo_u32 {r}, {r}, {k}"),
+    ("v_cmp_vcc_cndmask", "v_cmp_gt_u32 vcc, {r}, {k}\\nv_cndmask_b32 {r}, {r}, {k}, vcc"),
+    ("v_cmp_vcc_add", "v_cmp_gt_u32 vcc, {r}, {k}\\nv_add_u32 {r}, {r}, {k}"),
 ]
 
 head = r'''// GENERATED by tools/ubench/gen_valu_rates2.py -- see there.

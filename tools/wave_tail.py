@@ -42,17 +42,22 @@ def main():
     blk = []
     for bi in range(nb):
         ws = []
-        for w in range(8):
+        for w in range(16):
+            if buf[2 * (bi * 16 + w) + 1] == 0:  # (8-wave workgroups record waves 0..7 only)
+                continue
             hw = buf[2 * (bi * 16 + w)]
             d = buf[2 * (bi * 16 + w) + 1] / 100.0  # us (100 MHz)
             simd, cu, sh, se, xcc = (hw >> 4) & 3, (hw >> 8) & 15, (hw >> 12) & 1, (hw >> 13) & 7, (hw >> 32) & 15
             dur[w].append(d)
             ws.append(d)
             cu_waves[(xcc, se, sh, cu)].append((bi, w, simd, d))
-        blk.append(max(ws))
+        if ws:  # (chain mode: one block per CU, fewer blocks than frames)
+            blk.append(max(ws))
     print("mean duration by wave (us):", {w: round(statistics.mean(v), 1) for w, v in sorted(dur.items())})
     print("block duration (us): median %.1f max %.1f min %.1f" % (statistics.median(blk), max(blk), min(blk)))
-    if r.wl["kind"] == "fixtures":  # slot i holds fixture i mod len(fixtures)
+    q = sorted(blk)
+    print("block duration deciles (us):", [round(q[min(len(q) - 1, int(len(q) * k / 10))], 1) for k in range(11)])
+    if r.wl["kind"] == "fixtures" and len(blk) == nb:  # slot i holds fixture i mod len(fixtures)
         nf = len(r.wl["fixtures"])
         print("block duration by fixture (us, median):",
               {r.wl["fixtures"][k]: round(statistics.median(blk[k::nf]), 1) for k in range(nf)})

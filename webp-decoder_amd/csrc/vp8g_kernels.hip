@@ -274,7 +274,14 @@ DEV uint64_t vsel(bool c, uint64_t a, uint64_t b) {
 // step to be acknowledged: a full drain of the store queue per step, ~10 % of the kernel time.)
 typedef __amdgpu_buffer_rsrc_t Rsrc;
 constexpr uint32_t kNoStore = 0x80000000u;
-DEV Rsrc plane_rsrc(uint8_t* base, uint32_t bytes) { return __builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)bytes, 0x00020000); }
+DEV Rsrc plane_rsrc(uint8_t* base, uint32_t bytes) {
+	// (inputs laundered through readfirstlane: built inside the chain's frame loop, the resource was
+	// otherwise kept in VGPRs and every store became a waterfall loop)
+	const uint64_t b = (uint64_t)(uintptr_t)base;
+	const uint64_t bu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(b >> 32)) << 32) |
+	                    (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
+	return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)bu, (short)0, __builtin_amdgcn_readfirstlane((int)bytes), 0x00020000);
+}
 DEV void bst128(Rsrc r, uint32_t off, u32x4 v) { __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, 0); }
 DEV void bst64(Rsrc r, uint32_t off, u32x2 v) { __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)off, 0, 0); }
 
@@ -774,22 +781,35 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 	};
 	// chain mode: list index of the wave's current frame, its first global pair, and the last global
 	// pair (with its step count) of the frames one and two list positions back
-	uint32_t jf = 0, gbase = 0, last1 = ~0u, T1 = 0, last2 = ~0u, T2 = 0;
+	// (Only these few scalars are carried around the chain's frame loop; every other frame value is
+	// re-derived per pair from the laundered frame index: frame values carried as loop PHIs were
+	// taken for divergent, kept in VGPRs, and every output store became a waterfall loop.)
+	uint32_t jf = 0, gbase = 0, fcur = f, np_c = npairs;
+	auto uni = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
+	auto pairs_of = [&](uint32_t fi) { return (descs[fi].mb_rows + 1u) >> 1; };
 	for (uint32_t g = gw;; g += GW) {
 		uint32_t k;
 		if constexpr (kC) {
-			while (g >= gbase + npairs) {  // advance to the frame holding global pair g
-				last2 = last1, T2 = T1;
-				last1 = gbase + npairs - 1u, T1 = 2u * npairs - 1u < R ? CP2 : C;
-				gbase += npairs;
+			while (g >= gbase + np_c) {  // advance to the frame holding global pair g
+				gbase += np_c;
 				if (++jf >= m_chain) break;
-				set_frame((uint32_t)__builtin_amdgcn_readfirstlane((int)chain_list[jf]), jf & 1u);
+				fcur = uni(chain_list[jf]);
+				np_c = pairs_of(fcur);
 			}
 			if (jf >= m_chain) break;
+			jf = uni(jf), gbase = uni(gbase), fcur = uni(fcur);
+			set_frame(fcur, jf & 1u);
 			k = g - gbase;
 			if (k == 0) {
-				// claim slot jf & 1: frame jf - 2 must be done with it, then this frame's tables
-				if (last2 != ~0u && !dead) wait_prog(last2 % NW, (last2 << kProgShift) + T2, false);
+				// claim slot jf & 1: frame jf - 2 must be done with it, i.e. its last pair (global
+				// index gbase - pairs(jf - 1) - 1) must have published all T2 of its steps
+				if (jf >= 2 && !dead) {
+					const uint32_t f2 = uni(chain_list[jf - 2u]);
+					const uint32_t last2 = gbase - pairs_of(uni(chain_list[jf - 1u])) - 1u;
+					const uint32_t np2 = pairs_of(f2), R2 = descs[f2].mb_rows, C2 = descs[f2].mb_cols;
+					const uint32_t T2 = 2u * np2 - 1u < R2 ? C2 + 2u : C2;
+					wait_prog(last2 % NW, (last2 << kProgShift) + T2, false);
+				}
 				put_tables(*Dp, tabo, lane0);
 				wave_lds_sync();
 			} else if (!dead) {
