@@ -249,6 +249,16 @@ DEV uint32_t pk_clamp255(uint32_t x) {  // each int16 half clamped to [0, 255] (
 	v = __builtin_elementwise_min(__builtin_elementwise_max(v, s16x2{0, 0}), s16x2{255, 255});
 	return __builtin_bit_cast(uint32_t, v);
 }
+// both int16 halves of x saturated to u8, in bytes 0 / 1 (v_sat_pk_u8_i16, one VOP1 instead of the
+// v_pk_max_i16 + v_pk_min_i16 clamp and a byte-gathering v_perm)
+DEV uint32_t sat_pk(uint32_t x) {
+	uint32_t r;
+	asm("v_sat_pk_u8_i16 %0, %1" : "=v"(r) : "v"(x));
+	return r;
+}
+#ifndef VP8G_SATPK
+#define VP8G_SATPK 0
+#endif
 DEV int lo_s16(uint32_t x) { return (int)(int16_t)(x & 0xFFFFu); }
 DEV int hi_s16(uint32_t x) { return (int)(int16_t)(x >> 16); }
 DEV uint32_t pack2(int a, int b) { return __builtin_amdgcn_perm((uint32_t)b, (uint32_t)a, 0x05040100u); }
@@ -1140,21 +1150,22 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					const uint32_t A23 = pk_add(__builtin_amdgcn_perm(aw, aw, 0x0C030C02u) & mA, K2);
 					uint32_t wv[4];
 					// only TM_PRED's predictor can leave [0, 255]: its clamp runs when some lane uses it
+					// (VP8G_SATPK: the final clamp + byte packing by two v_sat_pk_u8_i16 and one shift-or)
+					auto pack_row = [&](uint32_t q01, uint32_t q23) -> uint32_t {
+						if constexpr (VP8G_SATPK) return sat_pk(q01) | (sat_pk(q23) << 16);
+						else return __builtin_amdgcn_perm(pk_clamp255(q23), pk_clamp255(q01), 0x06040200u);
+					};
 					if (__ballot(mode == 3) != 0ull) {
 #pragma unroll
 						for (int rr = 0; rr < 4; rr++) {
 							const uint32_t L2 = __builtin_amdgcn_perm(lw, lw, 0x0C000C00u + 0x00010001u * rr) & mL;
-							const uint32_t p01 = pk_clamp255(pk_add(pk_clamp255(pk_add(L2, A01)), rw[2 * rr]));
-							const uint32_t p23 = pk_clamp255(pk_add(pk_clamp255(pk_add(L2, A23)), rw[2 * rr + 1]));
-							wv[rr] = __builtin_amdgcn_perm(p23, p01, 0x06040200u);
+							wv[rr] = pack_row(pk_add(pk_clamp255(pk_add(L2, A01)), rw[2 * rr]), pk_add(pk_clamp255(pk_add(L2, A23)), rw[2 * rr + 1]));
 						}
 					} else {
 #pragma unroll
 						for (int rr = 0; rr < 4; rr++) {
 							const uint32_t L2 = __builtin_amdgcn_perm(lw, lw, 0x0C000C00u + 0x00010001u * rr) & mL;
-							const uint32_t p01 = pk_clamp255(pk_add(pk_add(L2, A01), rw[2 * rr]));
-							const uint32_t p23 = pk_clamp255(pk_add(pk_add(L2, A23), rw[2 * rr + 1]));
-							wv[rr] = __builtin_amdgcn_perm(p23, p01, 0x06040200u);
+							wv[rr] = pack_row(pk_add(pk_add(L2, A01), rw[2 * rr]), pk_add(pk_add(L2, A23), rw[2 * rr + 1]));
 						}
 					}
 #pragma unroll
