@@ -161,3 +161,52 @@ print(rc, C.get_errno(), round(time.time() - t, 3), lib.vp8g_last_error().decode
     assert int(rc) == -1 and int(err) == 5, r.stdout  # EIO
     assert "status" in " ".join(msg)
     assert float(secs) < 10.0, r.stdout
+
+
+def test_chain_many_small_mixed_frames_and_empty_slots(vp8g):
+    """Chain mode (vp8g_kernels.hip: one 16-wave workgroup per CU decodes a cost-sorted list of
+    frames as one chain of MB row pairs, two LDS context slots reused every other frame): 1 800
+    slots, ~7 frames per workgroup, of 48 distinct synthetic frames from 1x1 to 160x96 -- single-MB
+    and single-row frames (a pair of one row), odd sizes, all synthetic profiles (segments,
+    loop-filter deltas, simple and normal filter, +-2114 coefficients) -- in a scrambled order with
+    one slot in eight left empty (an all-zero descriptor: no work).  Every decoded slot must equal
+    the oracle's output for its frame and the empty slots' outputs must stay untouched."""
+    import vp8g_batch
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(11)
+    # (the two wide frames make the context slots large enough for the in-kernel cost sort)
+    sizes = [(1, 1), (16, 16), (17, 9), (160, 16), (33, 47), (160, 96), (1024, 16), (8, 96), (1000, 40)]
+    frames = []
+    for i in range(48):
+        w, h = sizes[i % len(sizes)]
+        frames.append(vp8g.synth_frame(w, h, 0xC4A1 ^ i, profile=i % 3))
+    n = 1800
+    b = vp8g_batch.DeviceBatch(n, 1024, 96, dev)
+    b.out.fill_(0xA5)
+    pick = rng.integers(0, len(frames), n)
+    empty = set(rng.choice(n, n // 8, replace=False).tolist())
+    for i in range(n):
+        if i not in empty:
+            b.place(i, frames[pick[i]], bool(pick[i] % 2))
+    b.commit()
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    b.launch(stream)
+    torch.cuda.synchronize()
+    assert b.status_word() == 0
+    exp = {}
+    bad = []
+    for i in range(n):
+        if i in empty:
+            continue
+        j = int(pick[i])
+        key = (j, bool(j % 2))
+        if key not in exp:
+            exp[key] = vp8g.oracle_reconstruct(frames[j], bool(j % 2))
+        got = b.frame_output(i)[:len(exp[key])]
+        if got != exp[key]:
+            bad.append(i)
+    assert not bad, f"{len(bad)} of {n - len(empty)} slots differ, e.g. {bad[:8]}"
+    for i in sorted(empty)[:16]:
+        assert b.frame_output(i) == b"\xa5" * b.i420, i
+    for f in frames:
+        f.free()

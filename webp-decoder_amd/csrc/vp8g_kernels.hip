@@ -257,7 +257,7 @@ DEV uint32_t sat_pk(uint32_t x) {
 	return r;
 }
 #ifndef VP8G_SATPK
-#define VP8G_SATPK 0
+#define VP8G_SATPK 1
 #endif
 DEV int lo_s16(uint32_t x) { return (int)(int16_t)(x & 0xFFFFu); }
 DEV int hi_s16(uint32_t x) { return (int)(int16_t)(x >> 16); }
