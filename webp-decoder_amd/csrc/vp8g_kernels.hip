@@ -56,6 +56,15 @@ constexpr int kPrioTab[11] = {VP8G_PRIO_TABLE, VP8G_PRIO_LF, VP8G_PRIO_WHT};
 #ifndef VP8G_LAUNDER  // step loop: invariant per-lane words and frame flags re-laundered every step
 #define VP8G_LAUNDER 1
 #endif
+#ifndef VP8G_FAST_FLUSH  // flush: per-pair folded store offsets for whole-piece frames (fl_fast)
+#define VP8G_FAST_FLUSH 1
+#endif
+#ifndef VP8G_FAST_STRIP  // borders: the filter-state copy of lanes 20..31 from kBorderTab roles
+#define VP8G_FAST_STRIP 1
+#endif
+#ifndef VP8G_COMPACT  // iDCT: blocks with AC compacted two lanes per block when at most 32 in the wave
+#define VP8G_COMPACT 0
+#endif
 #ifndef VP8G_LF_SELECT  // loop filter: masked filter input by select instead of a branch (sel0)
 #define VP8G_LF_SELECT 0
 #endif
@@ -185,7 +194,15 @@ constexpr BorderTab make_bordertab() {
 		} else if (ln < 17) t.v[ln] = BE(kLeft + 4 * (ln - 9), 0, 1);
 		else if (ln == 17) t.v[ln] = BE(kAbY + 12, 19, 2);  // corner P from the old abY[31]
 		else if (ln < 20) t.v[ln] = BE(kAbUV + 4 + 16 * (ln - 18), 11, 2);  // from abUV[15] / abUV[31]
-		else t.v[ln] = BE(0, 0, 3);
+		else {
+			// ln 20..31: copy of the MB above's filter-state rows (ctx_lf) into the tile -- luma rows
+			// 0..3 (ln 20..23, 16 B, bit 22) or U / V rows 0..3 (8 B): tile offset at slot 0 (slot 1:
+			// +16 / +8), source offset in the context column
+			const bool ly = ln < 24;
+			const int tr = ly ? ln - 20 : (ln - 24) & 3, p = (ln - 24) >> 2;
+			t.v[ln] = BE(ly ? kLfY + tr * kTP : kLfUV + p * kCV + tr * kTP, kCtxRecBytes + (ly ? tr * 16 : 64 + p * 32 + tr * 8), 3) |
+			          (ly ? 1u << 22 : 0u);
+		}
 	}
 	return t;
 }
@@ -284,6 +301,7 @@ DEV uint64_t vsel(bool c, uint64_t a, uint64_t b) {
 // step to be acknowledged: a full drain of the store queue per step, ~10 % of the kernel time.)
 typedef __amdgpu_buffer_rsrc_t Rsrc;
 constexpr uint32_t kNoStore = 0x80000000u;
+constexpr uint32_t kFlCtxBias = 512u;  // (fast flush: keeps the per-lane ctx_lf offsets non-negative)
 DEV Rsrc plane_rsrc(uint8_t* base, uint32_t bytes) {
 	// (inputs laundered through readfirstlane: built inside the chain's frame loop, the resource was
 	// otherwise kept in VGPRs and every store became a waterfall loop)
@@ -869,7 +887,10 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 		// Per-lane flush geometry of this pair (loop-filtered frames): lane ln of a half stores
 		// luma tile row ln (0..19) and chroma plane ln / 12, tile row ln % 12 of some column;
 		// image row = MB row origin + tile row - 4 (negative rows wrap and fail the crop test).
-		uint32_t fl_offY, fl_offC, fl_bits;
+		uint32_t fl_offY, fl_offC, fl_bits, fl_srcY = 0u, fl_srcC = 0u;
+#if VP8G_FAST_FLUSH
+		const bool fl_fast = lf_on && W == 16u * C && ((yal | sy) & 15u) == 0 && ((ual | suv | vofs) & 7u) == 0;
+#endif
 		{
 			const int hh = lane0 >> 5, ln = lane0 & 31;
 			const uint32_t rr = rA + (uint32_t)hh;
@@ -883,6 +904,33 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			fl_bits = (row_ok && ln < 20 && prowY < H ? 1u : 0u) | (ln >= 16 && nlast ? 2u : 0u) |
 			          (((yal + fl_offY) & 15u) == 0 ? 4u : 0u) | (row_ok && ln < 24 && prowC < CH ? 8u : 0u) |
 			          (kc >= 8 && nlast ? 16u : 0u) | (((ual + fl_offC) & 7u) == 0 ? 32u : 0u);
+#if VP8G_FAST_FLUSH
+			// Whole-piece frames (fl_fast): every row piece of a column inside the frame is a full,
+			// aligned 16-B / 8-B store.  The offsets then fold the lane's column shift (the left MB for
+			// tile rows >= 4) in, and a lane that never stores to HBM this pair (outside the crop, or
+			// its rows go to ctx_lf) gets a base past the plane end: per step offset = base + t * 16
+			// (chroma t * 8), taken when the MB is active and the column exists.
+			// The tile source of a lane's piece, by column parity (slot = t & 1): even | odd << 16,
+			// relative to the wave's LDS area.  The ctx_lf destination of the rows the next MB row still
+			// filters (luma ln 16..19; chroma tile rows 8..11, marked by bit 30) at t = 0, replacing
+			// fl_bits, or ~0u: offset + t * 160 once the column exists.
+			if (fl_fast) {
+				const bool topY = ln < 4, topC = kc < 4;
+				const uint32_t sh = 2u * (uint32_t)hh + (topY ? 0u : 1u);
+				const uint32_t shc = 2u * (uint32_t)hh + (topC ? 0u : 1u);
+				const uint32_t hb = (uint32_t)(kHdrBytes + (hh ? kHalfBytes : 0));
+				const uint32_t sY = hb + kLfY + (uint32_t)ln * kTP, sC = hb + kLfUV + (uint32_t)(pc * kCV + kc * kTP);
+				fl_srcY = (sY + (topY ? 0u : 16u)) | ((sY + (topY ? 16u : 0u)) << 16);
+				fl_srcC = (sC + (topC ? 0u : 8u)) | ((sC + (topC ? 8u : 0u)) << 16);
+				// lf_off(t - 2hh - 1) - t * 160 + kFlCtxBias (>= 0: sh <= 3)
+				const uint32_t lc0 = kFlCtxBias - sh * (uint32_t)kCtxBytesPerCol + (uint32_t)kCtxRecBytes;
+				const uint32_t lcY = lc0 + ((uint32_t)ln - 16u) * 16u;
+				const uint32_t lcC = lc0 + 64u + (uint32_t)pc * 32u + ((uint32_t)kc - 8u) * 8u;
+				fl_offY = (fl_bits & 1u) && !(fl_bits & 2u) ? fl_offY - sh * 16u : kNoStore;
+				fl_offC = (fl_bits & 8u) && !(fl_bits & 16u) ? fl_offC - shc * 8u : kNoStore;
+				fl_bits = (fl_bits & 3u) == 3u ? lcY : ((fl_bits & 24u) == 24u ? (lcC | 0x40000000u) : ~0u);  // (bit 2 / 16 alone: lanes 20..31)
+			}
+#endif
 		}
 		// The step's 32 bytes per lane, loaded one step ahead.  One variable carried around the loop
 		// and reloaded right after its last use (the dequantisation), so no register copy -- which
@@ -905,6 +953,9 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			// would otherwise be hoisted as 64-bit lane masks, which exhaust the SGPRs and are spilled
 			// to VGPR lanes (a v_readlane pair, plus a hazard wait, per use per step).
 			asm volatile("" : "+v"(bt_l), "+v"(fl_bits), "+s"(flags_l));
+#if VP8G_FAST_FLUSH
+			asm volatile("" : "+v"(fl_srcY), "+v"(fl_srcC));
+#endif
 			const bool lf_on = (flags_l & VP8G_F_LOOPFILTER) != 0;
 			const bool simple = (flags_l & VP8G_F_SIMPLE) != 0;
 			const bool lf_only = (flags_l & VP8G_F_LF_ONLY) != 0;
@@ -991,32 +1042,80 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					if (ln < 16 && !bpred) w[0] = (w[0] & 0xFFFF0000u) | *(const uint16_t*)(hv + kWht + 2 * ln);
 					PRIO(0);
 				}
-				// inverse DCT (RFC 14.4), whole 4x4 block per lane; DC-only shortcut when no lane
-				// of the wave has an AC coefficient ((dc+4)>>3 everywhere, exact)
-				if (__ballot(anyac && ln < 24 && act) != 0ull) {
-					uint32_t o[8];
-#pragma unroll
-					for (int h = 0; h < 2; h++) {  // vertical pass, two columns per op
-						const uint32_t r0 = w[h], r1 = w[2 + h], r2 = w[4 + h], r3 = w[6 + h];
-						const uint32_t a1 = pk_add(r0, r2), b1 = pk_sub(r0, r2);
-						const uint32_t c1 = pk_sub(mul_s2(r1), mul_c2(r3)), d1 = pk_add(mul_c2(r1), mul_s2(r3));
-						o[h] = pk_add(a1, d1);
-						o[6 + h] = pk_sub(a1, d1);
-						o[2 + h] = pk_add(b1, c1);
-						o[4 + h] = pk_sub(b1, c1);
-					}
-#pragma unroll
-					for (int r = 0; r < 4; r++) {  // horizontal pass
-						const int x0 = lo_s16(o[2 * r]), x1 = hi_s16(o[2 * r]), x2 = lo_s16(o[2 * r + 1]), x3 = hi_s16(o[2 * r + 1]);
-						const int a1 = x0 + x2 + 4, b1 = x0 - x2 + 4;
-						const int c1 = mul_s(x1) - mul_c(x3), d1 = mul_c(x1) + mul_s(x3);
-						rs[2 * r] = pack2((a1 + d1) >> 3, (b1 + c1) >> 3);
-						rs[2 * r + 1] = pack2((b1 - c1) >> 3, (a1 - d1) >> 3);
-					}
-				} else {
+				// inverse DCT (RFC 14.4).  DC-only shortcut when no lane of the wave has an AC coefficient
+				// ((dc+4)>>3 everywhere, exact).  With at most 32 blocks with AC in the wave (VP8G_COMPACT)
+				// the blocks are compacted, two lanes per block: the AC lanes stage their coefficients in
+				// the wave's kResid areas (slot q = rank among the AC lanes, 32 B: column halves 0 and
+				// 1), lane j transforms column half j & 1 of slot j >> 1 (vertical pass), swaps row halves
+				// with its partner lane (DPP), runs the horizontal pass on two rows and stores them back;
+				// the AC lanes read their rows.  Else the whole block per lane.
+				const uint64_t mac = __ballot(anyac && ln < 24 && act);
+				auto dc_fill = [&]() {
 					const int d = (lo_s16(w[0]) + 4) >> 3;
 #pragma unroll
 					for (int i = 0; i < 8; i++) rs[i] = pack2(d, d);
+				};
+				auto hpass = [&](uint32_t lo, uint32_t hi, uint32_t& y0, uint32_t& y1) {  // one row
+					const int x0 = lo_s16(lo), x1 = hi_s16(lo), x2 = lo_s16(hi), x3 = hi_s16(hi);
+					const int a1 = x0 + x2 + 4, b1 = x0 - x2 + 4;
+					const int c1 = mul_s(x1) - mul_c(x3), d1 = mul_c(x1) + mul_s(x3);
+					y0 = pack2((a1 + d1) >> 3, (b1 + c1) >> 3);
+					y1 = pack2((b1 - c1) >> 3, (a1 - d1) >> 3);
+				};
+				auto vpass = [&](uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3, uint32_t* o) {  // two columns
+					const uint32_t a1 = pk_add(r0, r2), b1 = pk_sub(r0, r2);
+					const uint32_t c1 = pk_sub(mul_s2(r1), mul_c2(r3)), d1 = pk_add(mul_c2(r1), mul_s2(r3));
+					o[0] = pk_add(a1, d1);
+					o[3] = pk_sub(a1, d1);
+					o[1] = pk_add(b1, c1);
+					o[2] = pk_sub(b1, c1);
+				};
+				if (mac == 0ull) {
+					dc_fill();
+				} else if (VP8G_COMPACT && __popcll(mac) <= 32) {
+					uint8_t* const wvb = smem + kHdrBytes + wave * kWaveBytes;
+					auto slot = [&](uint32_t q) { return wvb + (q >> 4) * (uint32_t)kHalfBytes + kResid + (q & 15u) * 32u; };
+					const bool isac = (mac >> lane) & 1ull;
+					const uint32_t q = __builtin_amdgcn_mbcnt_hi((uint32_t)(mac >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mac, 0u));
+					if (isac) {
+						st128(slot(q), u32x4{w[0], w[2], w[4], w[6]});
+						st128(slot(q) + 16, u32x4{w[1], w[3], w[5], w[7]});
+					}
+					dc_fill();
+					wave_lds_sync();
+					{
+						const uint32_t jq = (uint32_t)lane >> 1;
+						const bool h = lane & 1;
+						uint8_t* const sp = slot(jq) + (h ? 16u : 0u);
+						const u32x4 in = ld128(sp);
+						uint32_t o[4];  // rows 0..3 of column half h
+						vpass(in.x, in.y, in.z, in.w, o);
+						// lane h = 0 keeps rows 0, 1 and takes columns 2, 3 of them from its partner; h = 1 rows 2, 3
+						const uint32_t rx = (uint32_t)__builtin_amdgcn_mov_dpp((int)(h ? o[0] : o[2]), 0xB1, 0xF, 0xF, false);
+						const uint32_t ry = (uint32_t)__builtin_amdgcn_mov_dpp((int)(h ? o[1] : o[3]), 0xB1, 0xF, 0xF, false);
+						uint32_t y0, y1, y2, y3;
+						hpass(h ? rx : o[0], h ? o[2] : rx, y0, y1);
+						hpass(h ? ry : o[1], h ? o[3] : ry, y2, y3);
+						st128(sp, u32x4{y0, y1, y2, y3});
+					}
+					wave_lds_sync();
+					if (isac) {
+						const u32x4 lo = ld128(slot(q)), hi = ld128(slot(q) + 16);
+						rs[0] = lo.x, rs[1] = lo.y, rs[2] = lo.z, rs[3] = lo.w;
+						rs[4] = hi.x, rs[5] = hi.y, rs[6] = hi.z, rs[7] = hi.w;
+					}
+					wave_lds_sync();
+				} else {
+					uint32_t o[8];
+#pragma unroll
+					for (int h = 0; h < 2; h++) {  // vertical pass, two columns per op
+						uint32_t oh[4];
+						vpass(w[h], w[2 + h], w[4 + h], w[6 + h], oh);
+#pragma unroll
+						for (int r = 0; r < 4; r++) o[2 * r + h] = oh[r];
+					}
+#pragma unroll
+					for (int r = 0; r < 4; r++) hpass(o[2 * r], o[2 * r + 1], rs[2 * r], rs[2 * r + 1]);  // horizontal pass
 				}
 				if (ln < 16) {
 					uint8_t* rp = hv + kResid + ln * 32;
@@ -1091,7 +1190,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					const bool clampc = ln == 4 && cu + 1 == C;
 					const uint32_t rsrc = rec_off(cu + ((ln == 4 && !clampc) ? 1u : 0u)) + (clampc ? 12u : ((bt >> 12) & 0xFFu));
 					const uint32_t ldv = ctx.rd(rsrc);
-					const uint32_t kind = bt >> 20;
+					const uint32_t kind = (bt >> 20) & 3u;
 					const uint32_t vabove = top ? 0x7F7F7F7Fu : (clampc ? __builtin_amdgcn_perm(ldv, ldv, 0x03030303u) : ldv);
 					// corner: at the left edge a constant, else the previous MB's above row's last byte
 					// (still in the above-row buffer: read before this step's stores replace it)
@@ -1100,13 +1199,22 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					const uint32_t v = kind == 0 ? vabove : (kind == 1 ? 0x81818181u : vcorner);
 					if (ln < 20 && (kind != 1 || c == 0)) st32(hv + (bt & 0xFFFu), v);
 				}
-				if (lf_on && !top && ln >= 20) {  // filter state of the MB above (both modes)
+				if (lf_on && !top && ln >= 20) {  // filter state of the MB above (both modes; roles in kBorderTab)
+#if VP8G_FAST_STRIP
+					const uint32_t bt = bt_l;
+					const bool ly = (bt >> 22) & 1u;
+					const uint32_t lo = rec_off(cu) + ((bt >> 12) & 0xFFu);
+					uint8_t* const td = hv + (bt & 0xFFFu) + (slot ? (ly ? 16u : 8u) : 0u);
+					if (ly) st64(td, ctx.rd64(lo)), st64(td + 8, ctx.rd64(lo + 8));
+					else stc64(td, ctx.rd64(lo));
+#else
 					const bool ly = ln < 24;
 					const int p = (ln - 24) >> 2, tr = ly ? ln - 20 : (ln - 24) & 3;
 					const uint32_t lo = lf_off(cu) + (ly ? tr * 16 : 64 + p * 32 + tr * 8);
 					uint8_t* const td = ly ? tY + tr * kTP + slot * 16 : tC + p * kCV + tr * kTP + slot * 8;
 					if (ly) st64(td, ctx.rd64(lo)), st64(td + 8, ctx.rd64(lo + 8));
 					else stc64(td, ctx.rd64(lo));
+#endif
 				}
 			}
 			wave_lds_sync();
@@ -1330,7 +1438,28 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					offC = vis && full ? off : kNoStore;
 					poffC = off, pcntC = vis && !full ? min(CW - colpx, 8u) : 0u;
 				}
-			} else {
+			}
+#if VP8G_FAST_FLUSH
+			else if (fl_fast) {
+				// whole-piece frame: the folded per-pair offsets and tile sources (see fl_fast); the rows
+				// the next MB row still filters go to ctx_lf instead (fl_bits = their ctx_lf offset)
+				const uint32_t sl16 = (t & 1u) << 4;  // slot = c & 1 = t & 1
+				uint8_t* const wv = smem + wave * kWaveBytes;
+				const bool okc = act && (ln < 4 || c > 0);
+				srcY = wv + __builtin_amdgcn_ubfe(fl_srcY, sl16, 16u);
+				yl0 = ld64(srcY), yl1 = ld64(srcY + 8);
+				const uint32_t lcx = fl_bits, t160 = t * (uint32_t)kCtxBytesPerCol - kFlCtxBias;
+				if (okc && lcx < 0x40000000u) ctx.wr128(lcx + t160, u32x4{yl0.x, yl0.y, yl1.x, yl1.y});
+				offY = okc ? fl_offY + t * 16u : kNoStore;
+				const int kr = ln < 12 ? ln : ln - 12;
+				const bool okcc = act && (kr < 4 || c > 0);
+				srcC = wv + __builtin_amdgcn_ubfe(fl_srcC, sl16, 16u);
+				cl0 = ldc64(srcC);
+				if (okcc && (int)lcx > 0x3FFFFFFF) ctx.wr64(lcx + (t160 - 0x40000000u), cl0);
+				offC = okcc ? fl_offC + t * 8u : kNoStore;
+			}
+#endif
+			else {
 				{  // luma: ln 0..3 the MB above's bottom rows (this column, final now); 4..19 the left MB
 					const bool top = ln < 4;
 					const uint32_t col = top ? cu : cu - 1;
