@@ -2,13 +2,15 @@
 caller-owned device buffers, then vp8g_frame_digests), every slot checked against the digest of the
 reference decoder's own I420 (tests/golden/digests.json).
 
-* 260 x 4K (> 256 CUs: the launcher picks the timed `frame_kernel<8, false, false>`, no split);
+* 260 x 4K (> 256 CUs: the timed chain kernel `frame_kernel<16, false, false, true>` with the
+  mirror split, two frames per workgroup at most);
 * 1100 x 1080p (the fhd4 workload's geometry);
 * 300 mixed 4K / 1080p frames in a scrambled order (the cost-balanced launch order);
 * 64 distinct synthetic 4K frames of the bench's synthetic batch (seed 0x5EED ^ i);
 * the digest kernel against the numpy restatement on odd sizes (tail words, unaligned lengths);
 * a stalled producer (test build lib/diag/libvp8g_stall.so: one wave never publishes, waits give
-  up after 20 ms) ends the call promptly with EIO instead of waiting once per step.
+  up after 20 ms) ends the call promptly with EIO instead of waiting once per step;
+* the chain with ~7 mixed small frames per workgroup, and the same forced into the mirror split.
 Reference path: src/m06_recon/vp8_recon.c:718 (vp8_reconstruct_keyframe_yuv_filtered).
 """
 import ctypes as C
@@ -210,3 +212,17 @@ def test_chain_many_small_mixed_frames_and_empty_slots(vp8g):
         assert b.frame_output(i) == b"\xa5" * b.i420, i
     for f in frames:
         f.free()
+
+
+def test_chain_mirror_split_forced(vp8g):
+    """Mirror split of the chain (vp8g_kernels.hip, kSegTop: a frame's top half decoded first by its
+    own workgroup, its bottom half last by the mirror workgroup from a context snapshot), forced on
+    for a batch of ~6 mixed small frames per workgroup (VP8G_SPLITCHAIN=1, tests/chain_split_check.py
+    in a child process), two launches (the flags' epoch advances), every slot against the oracle.
+    The bench's uhd4 batch takes the split by default (two 4K frames per CU): 260 x 4K above."""
+    import os
+    env = dict(os.environ, VP8G_SPLITCHAIN="1")
+    r = subprocess.run([sys.executable, str(ROOT / "tests" / "chain_split_check.py")], capture_output=True, text=True,
+                       timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip().endswith("OK"), r.stdout

@@ -114,8 +114,14 @@ uint32_t pick_order(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint32_t ns
 // frames, a context too wide for two LDS slots, or VP8G_CHAIN=0), and whether the frames are
 // placed by cost class (*ordered; needs the sort scratch to fit the context slots).
 uint32_t pick_chain(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint32_t ctx_cols, bool* ordered);
+// Mirror split of a chain launch (vp8g_kernels.hip, kSegTop): worth it for ordered batches of at most
+// two frames per workgroup (VP8G_SPLITCHAIN=0 / 1 forces it off / on), and the doubled list must fit.
+bool pick_chain_split(uint32_t n_frames, uint32_t ctx_cols, uint32_t workgroups, bool ordered);
+// split: `snap` holds n_frames * ctx_cols * kCtxBytesPerCol bytes, `flags` n_frames words that hold
+// no value equal to `epoch` (a per-launch counter) before the launch.
 hipError_t launch_chain(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const Vp8gBatchArrays& arrays, uint8_t* d_out,
-                        uint32_t ctx_cols, hipStream_t stream, uint32_t workgroups, bool ordered);
+                        uint32_t ctx_cols, hipStream_t stream, uint32_t workgroups, bool ordered, bool split = false,
+                        uint8_t* snap = nullptr, uint32_t* flags = nullptr, uint32_t epoch = 0);
 
 constexpr uint32_t kMaxSplit = 8;
 int device_cus();

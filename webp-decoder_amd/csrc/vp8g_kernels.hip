@@ -630,6 +630,18 @@ DEV uint32_t ordered_frame(const Vp8gFrameDesc* descs, uint32_t n, uint32_t F, u
 // in the prologue by wave 0 (stable counting sort over the cost classes in LDS scratch).
 // Progress words encode global pair * 2048 + steps done (C <= 1024, so steps <= 1026).
 constexpr uint32_t kProgShift = 11;
+// Mirror split (launch_chain with split, batches of at most two frames per workgroup): each frame is
+// cut at pair h = ceil(pairs / 2) into a top segment (pairs [0, h), decoded by the frame's own
+// workgroup, first in its list) and a bottom segment (pairs [h, pairs), decoded LAST by the mirror
+// workgroup W-1-b).  Every workgroup thus decodes half of its own frames and half of its mirror's,
+// which evens out the pairing of heavy and light frames (two 4K frames per CU cannot balance four
+// fixture kinds).  The top segment's last pair, after its last step, copies the frame's context
+// slot (the row above the bottom segment, C x 160 B) to a snapshot in device memory (sc1 stores,
+// drained) and stores the launch's epoch in the frame's flag; the bottom segment's first pair,
+// when it claims its slot, waits for that flag and copies the snapshot into the slot.  Tops never
+// wait across workgroups and bottoms come after every top of their list, so no cycle exists, and a
+// top finishes in the first half of its workgroup's work, long before its bottom starts.
+constexpr uint32_t kSegTop = 1u, kSegBottom = 2u, kSegMask = 0x3FFFFFFFu;  // list entry: frame | tag << 30
 
 template <int NW, bool kG, bool kS, bool kC>
 __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kernel(const Vp8gFrameDesc* __restrict__ descs, Vp8gBatchArrays A,
@@ -655,7 +667,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			uint32_t* const hist = (uint32_t*)ctx_base;  // scratch (the context slots, written later)
 			uint32_t* const sorted = hist + kCostClasses;
 			const uint64_t lt = (1ull << lane0) - 1ull;
-			if (ord_first) {
+			if (ord_first & 1u) {
 				for (int i = lane0; i < (int)kCostClasses; i += 64) hist[i] = 0u;
 				wave_lds_sync();
 				for (int pass = 0; pass < 2; pass++) {
@@ -688,24 +700,31 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					}
 				}
 			}
-			// snake positions of workgroup b (increasing in j), empty descriptors left out
+			// snake positions of workgroup b (increasing in j), empty descriptors left out.  Mirror
+			// split (ord_first bit 1): workgroup b decodes the top halves of its own frames, then the
+			// bottom halves of workgroup W-1-b's frames (entry tags, kSegTop / kSegBottom)
 			uint32_t cnt = 0;
-			for (uint32_t j0 = 0;; j0 += 64) {
-				const uint32_t j = j0 + (uint32_t)lane0;
-				const uint32_t pos = j * Wg + ((j & 1u) ? Wg - 1u - b : b);
-				const bool valid = pos < n;
-				if (__ballot(valid) == 0ull) break;
-				const uint32_t fi = valid ? (ord_first ? sorted[pos] : pos) : 0u;
-				const bool keep = valid && descs[fi].mb_cols != 0 && descs[fi].mb_rows != 0;
-				const uint64_t mk = __ballot(keep);
-				if (keep) chain_list[cnt + (uint32_t)__popcll(mk & lt)] = fi;
-				cnt += (uint32_t)__popcll(mk);
-			}
+			auto add_list = [&](uint32_t bb, uint32_t tag) {
+				for (uint32_t j0 = 0;; j0 += 64) {
+					const uint32_t j = j0 + (uint32_t)lane0;
+					const uint32_t pos = j * Wg + ((j & 1u) ? Wg - 1u - bb : bb);
+					const bool valid = pos < n;
+					if (__ballot(valid) == 0ull) break;
+					const uint32_t fi = valid ? ((ord_first & 1u) ? sorted[pos] : pos) : 0u;
+					const bool keep = valid && descs[fi].mb_cols != 0 && descs[fi].mb_rows != 0 && (tag != kSegBottom || descs[fi].mb_rows > 2u);
+					const uint64_t mk = __ballot(keep);
+					if (keep) chain_list[cnt + (uint32_t)__popcll(mk & lt)] = fi | (tag << 30);
+					cnt += (uint32_t)__popcll(mk);
+				}
+			};
+			const bool split = (ord_first & 2u) != 0;
+			add_list(b, split ? kSegTop : 0u);
+			if (split) add_list(Wg - 1u - b, kSegBottom);
 			if (lane0 == 0) *(uint32_t*)(smem + kMisc) = cnt;
 		}
 		__syncthreads();
 		m_chain = (uint32_t)__builtin_amdgcn_readfirstlane((int)*(const uint32_t*)(smem + kMisc));
-		f = m_chain ? (uint32_t)__builtin_amdgcn_readfirstlane((int)chain_list[0]) : 0u;
+		f = m_chain ? (uint32_t)__builtin_amdgcn_readfirstlane((int)chain_list[0]) & kSegMask : 0u;
 	} else {
 		f = kS ? blockIdx.x % nfr : (ord_first ? ordered_frame<NW * 64>(descs, nfr, ord_first, smem) : blockIdx.x);
 	}
@@ -807,48 +826,93 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 		}
 		asm volatile("" ::: "memory");
 	};
+	// (chain, mirror split) bounded wait until a bottom segment's snapshot flag holds this launch's epoch
+	auto wait_flag = [&](uint32_t* flag, uint32_t epoch) {
+		uint32_t spins = 0;
+		uint64_t t0 = 0;
+		while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+			__builtin_amdgcn_s_sleep(2);
+			if ((++spins & 255u) == 0) {
+				const uint64_t now = __builtin_amdgcn_s_memrealtime();
+				if (t0 == 0) t0 = now;
+				else if (now - t0 > (uint64_t)VP8G_WAIT_TICKS) {
+					if (lane0 == 0) atomicOr(A.status, VP8G_ERR_TIMEOUT);
+					dead = true;
+					break;
+				}
+			}
+		}
+		asm volatile("" ::: "memory");
+	};
+	auto uni = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
 	// chain mode: list index of the wave's current frame, its first global pair, and the last global
 	// pair (with its step count) of the frames one and two list positions back
 	// (Only these few scalars are carried around the chain's frame loop; every other frame value is
 	// re-derived per pair from the laundered frame index: frame values carried as loop PHIs were
 	// taken for divergent, kept in VGPRs, and every output store became a waterfall loop.)
-	uint32_t jf = 0, gbase = 0, fcur = f, np_c = npairs;
-	auto uni = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
+	// (chain: list entries carry a segment tag, see kSegTop; a segment is pairs [k0, k0 + its pairs))
 	auto pairs_of = [&](uint32_t fi) { return (descs[fi].mb_rows + 1u) >> 1; };
+	auto seg_k0 = [&](uint32_t e) { return (e >> 30) == kSegBottom ? (pairs_of(e & kSegMask) + 1u) >> 1 : 0u; };
+	auto seg_pairs = [&](uint32_t e) {
+		const uint32_t np = pairs_of(e & kSegMask), tag = e >> 30;
+		return tag == 0u ? np : (tag == kSegTop ? (np + 1u) >> 1 : np >> 1);
+	};
+	uint32_t jf = 0, gbase = 0, ecur = kC ? uni(chain_list[0]) : f, np_c = kC ? seg_pairs(ecur) : npairs;
 	for (uint32_t g = gw;; g += GW) {
 		uint32_t k;
+		bool has_pred;        // the pair above is decoded by this workgroup (else: frame top, or a bottom segment's snapshot)
+		bool snap_out = false;  // (kC) the top segment's last pair: context -> snapshot after its last step
+		uint32_t fcur = f;
 		if constexpr (kC) {
-			while (g >= gbase + np_c) {  // advance to the frame holding global pair g
+			while (g >= gbase + np_c) {  // advance to the segment holding global pair g
 				gbase += np_c;
 				if (++jf >= m_chain) break;
-				fcur = uni(chain_list[jf]);
-				np_c = pairs_of(fcur);
+				ecur = uni(chain_list[jf]);
+				np_c = seg_pairs(ecur);
 			}
 			if (jf >= m_chain) break;
-			jf = uni(jf), gbase = uni(gbase), fcur = uni(fcur);
+			jf = uni(jf), gbase = uni(gbase), ecur = uni(ecur);
+			fcur = ecur & kSegMask;
 			set_frame(fcur, jf & 1u);
-			k = g - gbase;
-			if (k == 0) {
-				// claim slot jf & 1: frame jf - 2 must be done with it, i.e. its last pair (global
+			const uint32_t tag = ecur >> 30, k0 = seg_k0(ecur);
+			k = k0 + (g - gbase);
+			has_pred = g > gbase;
+			snap_out = tag == kSegTop && g + 1u == gbase + np_c && np_c < npairs;
+			if (g == gbase) {
+				// claim slot jf & 1: segment jf - 2 must be done with it, i.e. its last pair (global
 				// index gbase - pairs(jf - 1) - 1) must have published all T2 of its steps
 				if (jf >= 2 && !dead) {
-					const uint32_t f2 = uni(chain_list[jf - 2u]);
-					const uint32_t last2 = gbase - pairs_of(uni(chain_list[jf - 1u])) - 1u;
-					const uint32_t np2 = pairs_of(f2), R2 = descs[f2].mb_rows, C2 = descs[f2].mb_cols;
-					const uint32_t T2 = 2u * np2 - 1u < R2 ? C2 + 2u : C2;
+					const uint32_t e2 = uni(chain_list[jf - 2u]), f2 = e2 & kSegMask;
+					const uint32_t last2 = gbase - seg_pairs(uni(chain_list[jf - 1u])) - 1u;
+					const uint32_t kl2 = seg_k0(e2) + seg_pairs(e2) - 1u, R2 = descs[f2].mb_rows, C2 = descs[f2].mb_cols;
+					const uint32_t T2 = 2u * kl2 + 1u < R2 ? C2 + 2u : C2;
 					wait_prog(last2 % NW, (last2 << kProgShift) + T2, false);
+				}
+				if (tag == kSegBottom) {
+					// the rows above come from the top segment's snapshot (another workgroup)
+					uint32_t* const flag = gprog + fcur;
+					if (!dead) wait_flag(flag, nsplit);
+					const uint8_t* const src = gctx + (size_t)fcur * slot_bytes;
+					for (uint32_t o = (uint32_t)lane0 * 16u; o < C * (uint32_t)kCtxBytesPerCol; o += 1024u) {
+						const uint32_t* q = (const uint32_t*)(src + o);
+						st128(ctx.lds + o, u32x4{__hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+						                         __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+						                         __hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+						                         __hip_atomic_load(q + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)});
+					}
 				}
 				put_tables(*Dp, tabo, lane0);
 				wave_lds_sync();
 			} else if (!dead) {
 				// step 0's dependency wait, before its residual: the residual reads the dequant table
-				// that pair 0 writes when it claims the slot (pair k - 1 past step 0 implies pair 0 past
-				// it, and pair 0 writes its tables before its first publish)
+				// that the segment's first pair writes when it claims the slot (pair g - 1 past step 0
+				// implies the first pair past it, and that pair writes its tables before its first publish)
 				wait_prog((uint32_t)((wave + NW - 1) % NW), ((g - 1u) << kProgShift) + 1u, false);
 			}
 		} else {
 			k = g;
 			if (k >= npairs) break;
+			has_pred = k > 0;
 		}
 		// output planes (built per pair: a buffer resource carried around the chain's frame loop
 		// would be a loop PHI the backend cannot keep in SGPRs)
@@ -1130,7 +1194,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 
 			// ---------------------------------------------- wait: pair k-1's lower row 2 cols ahead
 			PRIO(1);
-			if (k > 0 && !dead && !(VP8G_ABLATE & 8)) {
+			if (has_pred && !dead && !(VP8G_ABLATE & 8)) {
 				// (one column more lag across parts: the mailbox is read a step ahead of use)
 				const uint32_t lag = xin ? 5u : 4u;
 				const uint32_t ahead = (t + lag < CP2) ? t + lag : CP2;
@@ -1535,6 +1599,22 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			wave_lds_sync();
 			STAMP(6);
 
+			if (kC && snap_out && t + 1u == T) {
+				// top segment of a mirror-split frame, last step of its last pair: every column's context
+				// is final -> snapshot (write-through stores, drained) -> flag = this launch's epoch
+				asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+				uint8_t* const dst = gctx + (size_t)fcur * slot_bytes;
+				for (uint32_t o = (uint32_t)lane0 * 16u; o < C * (uint32_t)kCtxBytesPerCol; o += 1024u) {
+					const u32x4 v = ld128(ctx.lds + o);
+					uint32_t* q = (uint32_t*)(dst + o);
+					__hip_atomic_store(q, v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+					__hip_atomic_store(q + 1, v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+					__hip_atomic_store(q + 2, v.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+					__hip_atomic_store(q + 3, v.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+				}
+				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+				if (lane0 == 0) __hip_atomic_store(gprog + fcur, nsplit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			}
 			// ---------------------------------------------- publish progress
 			PRIO(7);
 			ctx.publish_fence();
@@ -1692,16 +1772,34 @@ uint32_t pick_chain(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint32_t ct
 	return wg;
 }
 
-hipError_t launch_chain(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const Vp8gBatchArrays& arrays, uint8_t* d_out,
-                        uint32_t ctx_cols, hipStream_t stream, uint32_t workgroups, bool ordered) {
-	if (n_frames == 0) return hipSuccess;
+bool pick_chain_split(uint32_t n_frames, uint32_t ctx_cols, uint32_t workgroups, bool ordered) {
+#ifndef VP8G_SPLITCHAIN_DEFAULT  // (A/B builds: -DVP8G_SPLITCHAIN_DEFAULT=0 / 1)
+#define VP8G_SPLITCHAIN_DEFAULT -1
+#endif
+	static const int mode = [] {  // VP8G_SPLITCHAIN=0: never, =1: whenever it fits (A/B experiments, tests)
+		const char* e = getenv("VP8G_SPLITCHAIN");
+		return e ? atoi(e) : VP8G_SPLITCHAIN_DEFAULT;
+	}();
+	if (mode == 0 || workgroups == 0) return false;
 	const uint32_t list_max = (n_frames + workgroups - 1) / workgroups;
-	const size_t lds = chain_lds_bytes(ctx_cols, list_max);
+	if (chain_lds_bytes(ctx_cols, 2 * list_max) > (size_t)kMaxLds) return false;
+	return mode > 0 || (ordered && list_max <= 2);
+}
+
+hipError_t launch_chain(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const Vp8gBatchArrays& arrays, uint8_t* d_out,
+                        uint32_t ctx_cols, hipStream_t stream, uint32_t workgroups, bool ordered, bool split, uint8_t* snap,
+                        uint32_t* flags, uint32_t epoch) {
+	if (n_frames == 0) return hipSuccess;
+	if (split && (!snap || !flags)) return hipErrorInvalidValue;
+	const uint32_t list_max = (n_frames + workgroups - 1) / workgroups;
+	const size_t lds = chain_lds_bytes(ctx_cols, split ? 2 * list_max : list_max);
 	auto fn = frame_kernel<kChainWaves, false, false, true>;
 	hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
 	if (e != hipSuccess) return e;
-	hipLaunchKernelGGL(fn, dim3(workgroups), dim3(kChainWaves * 64), lds, stream, d_descs, arrays, d_out, ctx_cols, nullptr, 1u,
-	                   nullptr, nullptr, ordered ? 1u : 0u, n_frames);
+	// (chain kernel arguments: gctx = snapshots, gprog = flags, nsplit = epoch, ord_first = ordered | split << 1)
+	hipLaunchKernelGGL(fn, dim3(workgroups), dim3(kChainWaves * 64), lds, stream, d_descs, arrays, d_out, ctx_cols,
+	                   split ? snap : nullptr, split ? epoch : 1u, nullptr, split ? flags : nullptr,
+	                   (ordered ? 1u : 0u) | (split ? 2u : 0u), n_frames);
 	return hipGetLastError();
 }
 

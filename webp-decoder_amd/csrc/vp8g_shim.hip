@@ -117,6 +117,11 @@ struct DevState {
 	size_t gctx_cap = 0;
 	uint8_t* mbox = nullptr;  // split-mode hand-off mailboxes + progress words (host APIs only)
 	size_t mbox_cap = 0;
+	uint8_t* snap = nullptr;  // mirror-split chain launches: per-frame context snapshots + flags
+	size_t snap_cap = 0;
+	uint8_t* sflags = nullptr;
+	size_t sflags_cap = 0;
+	uint32_t epoch = 0;  // launch counter for the snapshot flags
 	uint32_t* status = nullptr;
 };
 DevState g_dev;
@@ -224,7 +229,20 @@ int run_locked(const std::vector<Vp8gFrameDesc>& descs, const Vp8gBatchArrays& a
 		bool ordered = false;
 		const uint32_t wg = vp8g::pick_chain(descs.data(), n, max_cols, &ordered);
 		if (wg) {
-			HIP_TRY(vp8g::launch_chain((const Vp8gFrameDesc*)d_descs, n, arr, d_out, max_cols, s, wg, ordered), "launch");
+			// mirror split (vp8g_kernels.hip, kSegTop): snapshot buffers and a fresh epoch for the flags
+			const bool split = vp8g::pick_chain_split(n, max_cols, wg, ordered);
+			if (split) {
+				HIP_TRY(grow(&g_dev.snap, &g_dev.snap_cap, (size_t)n * max_cols * vp8g::kCtxBytesPerCol), "hipMalloc(snapshots)");
+				const size_t old_cap = g_dev.sflags_cap;
+				HIP_TRY(grow(&g_dev.sflags, &g_dev.sflags_cap, (size_t)n * sizeof(uint32_t)), "hipMalloc(flags)");
+				if (++g_dev.epoch == 0 || g_dev.sflags_cap != old_cap) {
+					if (g_dev.epoch == 0) g_dev.epoch = 1;
+					HIP_TRY(hipMemsetAsync(g_dev.sflags, 0, g_dev.sflags_cap, s), "memset(flags)");
+				}
+			}
+			HIP_TRY(vp8g::launch_chain((const Vp8gFrameDesc*)d_descs, n, arr, d_out, max_cols, s, wg, ordered, split, g_dev.snap,
+			                           (uint32_t*)g_dev.sflags, g_dev.epoch),
+			        "launch");
 			return 0;
 		}
 	}
