@@ -65,6 +65,12 @@ constexpr int kPrioTab[11] = {VP8G_PRIO_TABLE, VP8G_PRIO_LF, VP8G_PRIO_WHT};
 #ifndef VP8G_COMPACT  // iDCT: blocks with AC compacted two lanes per block when at most 32 in the wave
 #define VP8G_COMPACT 0
 #endif
+#ifndef VP8G_KATTR  // (experiments: e.g. __attribute__((amdgpu_num_vgpr(112))) to probe the register budget)
+#define VP8G_KATTR
+#endif
+#ifndef VP8G_FAST_LF  // loop filter: line addresses from per-pair lane words (lf_vp / lf_hp)
+#define VP8G_FAST_LF 1
+#endif
 #ifndef VP8G_LF_SELECT  // loop filter: masked filter input by select instead of a branch (sel0)
 #define VP8G_LF_SELECT 0
 #endif
@@ -491,10 +497,23 @@ DEV void gather20(const uint8_t* a, const uint8_t* b, int* px) {
 
 // Both passes of the loop filter over this lane's line of the MB held in LDS.  Lanes 0..15:
 // luma rows / columns; 16..23 U, 24..31 V.  Bytes that may change: 1..17 (luma), 1..9 (chroma).
-template <bool kSimple>
-DEV void lf_mb(uint8_t* tY, uint8_t* tC, int ln, int slot, bool en, bool mb_v, bool mb_h, bool inner, int E, int I, int T) {
+// The line addresses of a lane: Lp / Mp the left neighbour's 4 pixels / this MB's pixels of its
+// row (vertical-edge pass), colp the top of its column (horizontal-edge pass, tile row 0).
+struct LfLine {
+	uint8_t* Lp;
+	uint8_t* Mp;
+	uint8_t* colp;
+};
+DEV LfLine lf_lines(uint8_t* tY, uint8_t* tC, int ln, int slot) {
 	const bool isy = ln < 16;
 	const int cp = (ln >> 3) & 1;
+	uint8_t* const rowp = isy ? tY + (4 + ln) * kTP : tC + (4 + (ln & 7)) * kTP + cp * kCV;
+	const int off = isy ? slot * 16 : slot * 8, ring = isy ? 31 : 15;
+	return LfLine{rowp + ((off - 4) & ring), rowp + off, isy ? tY + slot * 16 + ln : tC + cp * kCV + slot * 8 + (ln & 7)};
+}
+template <bool kSimple>
+DEV void lf_mb(const LfLine& L, int ln, bool en, bool mb_v, bool mb_h, bool inner, int E, int I, int T) {
+	const bool isy = ln < 16;
 	const bool wr = en && (isy || !kSimple);
 	int px[20];
 	// vertical edges: one line per lane along a pixel row; the neighbour's 4 pixels sit at the
@@ -502,10 +521,8 @@ DEV void lf_mb(uint8_t* tY, uint8_t* tC, int ln, int slot, bool en, bool mb_v, b
 	{
 		// (ldb/stb: relaxed wave-scope atomics keep the byte accesses single ds_read_u8 /
 		// ds_write_b8 -- merged wide accesses cost vector instructions to (un)pack)
-		uint8_t* const rowp = isy ? tY + (4 + ln) * kTP : tC + (4 + (ln & 7)) * kTP + cp * kCV;
-		const int off = isy ? slot * 16 : slot * 8, ring = isy ? 31 : 15;
-		uint8_t* const Lp = rowp + ((off - 4) & ring);
-		uint8_t* const Mp = rowp + off;
+		uint8_t* const Lp = L.Lp;
+		uint8_t* const Mp = L.Mp;
 		PRIO(8);
 		gather20<1, 1>(Lp, Mp, px);
 		PRIO(9);
@@ -524,7 +541,7 @@ DEV void lf_mb(uint8_t* tY, uint8_t* tC, int ln, int slot, bool en, bool mb_v, b
 	wave_lds_sync();
 	// horizontal edges: one line per lane down a pixel column (tile rows 0..19, pitch kTP)
 	{
-		uint8_t* const colp = isy ? tY + slot * 16 + ln : tC + cp * kCV + slot * 8 + (ln & 7);
+		uint8_t* const colp = L.colp;
 		PRIO(8);
 		gather20<kTP, kTP>(colp, colp + 4 * kTP, px);
 		PRIO(9);
@@ -644,7 +661,7 @@ constexpr uint32_t kProgShift = 11;
 constexpr uint32_t kSegTop = 1u, kSegBottom = 2u, kSegMask = 0x3FFFFFFFu;  // list entry: frame | tag << 30
 
 template <int NW, bool kG, bool kS, bool kC>
-__global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kernel(const Vp8gFrameDesc* __restrict__ descs, Vp8gBatchArrays A,
+__global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void frame_kernel(const Vp8gFrameDesc* __restrict__ descs, Vp8gBatchArrays A,
                                                         uint8_t* __restrict__ out, uint32_t ctx_cols,
                                                         uint8_t* __restrict__ gctx, uint32_t nsplit,
                                                         uint8_t* __restrict__ mbox, uint32_t* __restrict__ gprog,
@@ -952,6 +969,21 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 		// luma tile row ln (0..19) and chroma plane ln / 12, tile row ln % 12 of some column;
 		// image row = MB row origin + tile row - 4 (negative rows wrap and fail the crop test).
 		uint32_t fl_offY, fl_offC, fl_bits, fl_srcY = 0u, fl_srcC = 0u;
+#if VP8G_FAST_LF
+		// loop-filter line addresses of this lane (see lf_lines), relative to the wave's LDS area:
+		// slot 0 in bits 0..15, slot 1 in 16..31
+		uint32_t lf_vp, lf_hp;
+		{
+			const int hh = lane0 >> 5, ln = lane0 & 31;
+			const bool isy = ln < 16;
+			const uint32_t cp = (uint32_t)(ln >> 3) & 1u, hb = (uint32_t)(kHdrBytes + (hh ? kHalfBytes : 0));
+			const uint32_t rowp = hb + (isy ? (uint32_t)(kLfY + (4 + ln) * kTP) : (uint32_t)kLfUV + (4u + (uint32_t)(ln & 7)) * kTP + cp * kCV);
+			const uint32_t col = hb + (isy ? (uint32_t)(kLfY + ln) : (uint32_t)kLfUV + cp * kCV + (uint32_t)(ln & 7));
+			const uint32_t d = isy ? 16u : 8u;
+			lf_vp = rowp | ((rowp + d) << 16);
+			lf_hp = col | ((col + d) << 16);
+		}
+#endif
 #if VP8G_FAST_FLUSH
 		const bool fl_fast = lf_on && W == 16u * C && ((yal | sy) & 15u) == 0 && ((ual | suv | vofs) & 7u) == 0;
 #endif
@@ -1019,6 +1051,9 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			asm volatile("" : "+v"(bt_l), "+v"(fl_bits), "+s"(flags_l));
 #if VP8G_FAST_FLUSH
 			asm volatile("" : "+v"(fl_srcY), "+v"(fl_srcC));
+#endif
+#if VP8G_FAST_LF
+			asm volatile("" : "+v"(lf_vp), "+v"(lf_hp));
 #endif
 			const bool lf_on = (flags_l & VP8G_F_LOOPFILTER) != 0;
 			const bool simple = (flags_l & VP8G_F_SIMPLE) != 0;
@@ -1431,8 +1466,21 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 				const bool en = act && E != 0;
 				if (__ballot(en) != 0ull) {
 					const bool inner = hasc != 0 || bpred;
-					if (simple) lf_mb<true>(tY, tC, ln, slot, en, c > 0, r > 0, inner, E, I, Tt);
-					else lf_mb<false>(tY, tC, ln, slot, en, c > 0, r > 0, inner, E, I, Tt);
+#if VP8G_FAST_LF
+					// (per-pair lane words: tile offsets at slot 0 | slot 1 << 16, from the wave's area)
+					LfLine L;
+					{
+						const uint32_t sl16 = (t & 1u) << 4;
+						uint8_t* const wv = smem + wave * kWaveBytes;
+						L.Mp = wv + __builtin_amdgcn_ubfe(lf_vp, sl16, 16u);
+						L.Lp = L.Mp + (slot ? -4 : (ln < 16 ? 28 : 12));
+						L.colp = wv + __builtin_amdgcn_ubfe(lf_hp, sl16, 16u);
+					}
+#else
+					const LfLine L = lf_lines(tY, tC, ln, slot);
+#endif
+					if (simple) lf_mb<true>(L, ln, en, c > 0, r > 0, inner, E, I, Tt);
+					else lf_mb<false>(L, ln, en, c > 0, r > 0, inner, E, I, Tt);
 				}
 			}
 			STAMP(5);
