@@ -46,7 +46,11 @@ constexpr int kProgress = 0;      // 16 x u32 progress words (one per wave)
 constexpr int kBpTable = 64;      // B_PRED predictor table: 11 modes x 16 px x {perm selectors, byte
                                   // mask, dot weights, bias | shift}
 constexpr int kBpModes = 11;      // modes 0..9 + one constant-128 entry for out-of-range modes
-constexpr int kDqTable = kBpTable + kBpModes * 16 * 16;  // 4 segments x 6 int16 dequant factors
+#ifndef VP8G_BP_DCFOLD  // B_PRED: DC_PRED folded into the table's dot product (32-B entries)
+#define VP8G_BP_DCFOLD 0
+#endif
+constexpr int kBpEntry = VP8G_BP_DCFOLD ? 32 : 16;  // bytes per (mode, pixel) entry
+constexpr int kDqTable = kBpTable + kBpModes * 16 * kBpEntry;  // 4 segments x 6 int16 dequant factors
 constexpr int kLfTable = kDqTable + 48;                 // 4 segments x 2 (B_PRED?) x {E, I, T, 0}
 constexpr int kTabStride = 80;                          // per frame slot (chain mode: two slots)
 constexpr int kMisc = kDqTable + 2 * kTabStride;        // chain mode: list length

@@ -129,7 +129,7 @@ constexpr int kBS = 4 * kTP - 8;  // B_PRED: tile offset from sub-block (i, j) t
 // Edge index notation of the builders: 0..3 = L3..L0, 4 = P, 5..12 = A0..A7.
 // ---------------------------------------------------------------------------------------------
 struct BpTab {
-	uint32_t v[kBpModes * 16 * 4];
+	uint32_t v[kBpModes * 16 * (kBpEntry / 4)];
 };
 constexpr int epos(int e) { return e < 4 ? 3 - e : (e == 4 ? 7 : e + 3); }
 struct Tri {
@@ -174,10 +174,25 @@ constexpr BpTab make_bptab() {
 			// weights (signed bytes) and bias / shift of the one dot-product formula:
 			// value = (sdot4(E_xyz - 128, w) + bias) >> sh  (avg3: (1, 2, 1), 514, 2; TM: (1, -1, 1), 128, 0)
 			const bool tm = m == 1;
+#if VP8G_BP_DCFOLD
+			// 32-B entry {sel, byte mask, weights, bias, shift, above-row mask, 0, 0}: DC_PRED is the dot
+			// of the four left bytes (selectors 0..3, weights 1) plus a v_sad_u8 of the four above bytes
+			// under the above-row mask, (sum + 4) >> 3; every other mode masks the above row to zero
+			const bool dc = m == 0;
+			uint32_t* const en = &t.v[(m * 16 + p) * 8];
+			en[0] = dc ? 0x03020100u : sel;
+			en[1] = dc ? 0u : mask;
+			en[2] = dc ? 0x01010101u : (tm ? 0x0001FF01u : 0x00010201u);
+			en[3] = dc ? 516u : (tm ? 128u : 514u);
+			en[4] = dc ? 3u : (tm ? 0u : 2u);
+			en[5] = dc ? 0xFFFFFFFFu : 0u;
+			en[6] = en[7] = 0u;
+#else
 			t.v[(m * 16 + p) * 4] = sel;
 			t.v[(m * 16 + p) * 4 + 1] = mask | ((tm ? 0u : 2u) << 24);  // byte 3: the shift (x3's byte 3 is unused)
 			t.v[(m * 16 + p) * 4 + 2] = tm ? 0x0001FF01u : 0x00010201u;
 			t.v[(m * 16 + p) * 4 + 3] = tm ? 128u : 514u;
+#endif
 		}
 	return t;
 }
@@ -747,7 +762,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 	}
 	const uint32_t part = kS ? blockIdx.x / nfr : 0u;
 
-	for (int i = (int)threadIdx.x; i < kBpModes * 64; i += NW * 64) ((uint32_t*)(smem + kBpTable))[i] = kBpTab.v[i];
+	for (int i = (int)threadIdx.x; i < kBpModes * 16 * (kBpEntry / 4); i += NW * 64) ((uint32_t*)(smem + kBpTable))[i] = kBpTab.v[i];
 	uint32_t bt_l = kBorderTab.v[lane0 & 31];  // this lane's border-setup role (loop-invariant)
 	// dequant / loop-filter tables of a frame into its slot (chain mode: by the wave of the frame's pair 0)
 	auto put_tables = [&](const Vp8gFrameDesc& Df, uint32_t tabo, int l) {
@@ -1407,7 +1422,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 					const uint8_t* const aE = g ? tA : abY + 16;                              // i0 == 0: + 4 s
 					uint8_t* const lB = left + 36 * g;                                        // + 36 i0 - 16 s
 					const int16_t* const rsp = (const int16_t*)(hv + kResid) + p + 32 * g;    // + 16 b0
-					const u32x4* const tabp = (const u32x4*)(smem + kBpTable) + p;            // + 16 mode
+					const u32x4* const tabp = (const u32x4*)(smem + kBpTable) + p * (kBpEntry / 16);  // + 16 mode entries
 					const bool col3 = cc == 3;
 #pragma unroll
 					for (int s = 0; s < 10; s++) {
@@ -1428,17 +1443,25 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 							const uint8_t* const pp = i0 == 0 ? (g ? lb - 1 : arow - 1) : lb - 1;
 							const uint32_t a03 = ld32(arow), a47 = ld32(a47p), lw = ld32(lb);
 							const uint32_t pv = *pp;
-							const u32x4 tb = tabp[16 * mode];
+							const u32x4 tb = tabp[16 * (kBpEntry / 16) * mode];
 							const int rv = rsp[16 * b0];
 							const uint32_t ey = (pv << 24) | 0x808080u;
 							const uint32_t lo = __builtin_amdgcn_perm(ey, lw, tb.x);
 							const uint32_t hi = __builtin_amdgcn_perm(a47, a03, tb.x);
 							const uint32_t x3 = (hi & tb.y) | (lo & ~tb.y);  // bytes 0..2 = x, y, z
+#if VP8G_BP_DCFOLD
+							// every mode in one signed dot product over the byte-biased edge, DC_PRED's above row
+							// added by v_sad_u8 under the entry's mask
+							const u32x4 tb2 = tabp[16 * (kBpEntry / 16) * mode + 1];
+							const int dot = __builtin_amdgcn_sdot4((int)(x3 ^ 0x80808080u), (int)tb.z, (int)tb.w, false);
+							const int pred = sat8((int)__builtin_amdgcn_sad_u8(a03 & tb2.y, 0u, (uint32_t)dot) >> tb2.x);
+#else
 							// directional modes and TM in one signed dot product over the byte-biased edge
 							const int vdir = sat8(__builtin_amdgcn_sdot4((int)(x3 ^ 0x00808080u), (int)tb.z, (int)tb.w, false) >>
 							                      (tb.y >> 24));
 							const int vdc = (int)((__builtin_amdgcn_sad_u8(a03, 0u, __builtin_amdgcn_sad_u8(lw, 0u, 4u))) >> 3);
 							const int pred = mode == 0 ? vdc : vdir;
+#endif
 							const int px = sat8(pred + rv);
 							tpix[kBS * i0 + 4 * s] = (uint8_t)px;
 							// right pixel column of a sub-block: left column of the next sub-block column (in
