@@ -22,7 +22,7 @@ namespace vp8g {
 #define VP8G_UV 804
 #endif
 #ifndef VP8G_CV
-#define VP8G_CV 16
+#define VP8G_CV 64
 #endif
 constexpr int kTP = VP8G_TP;    // tile row pitch
 constexpr int kLfY = 0;         // luma filter tile: 20 rows x kTP (4 rows above + 16 MB rows; two MB
@@ -30,8 +30,13 @@ constexpr int kLfY = 0;         // luma filter tile: 20 rows x kTP (4 rows above
 constexpr int kLfUV = VP8G_UV;  // chroma tile: 12 rows x kTP (4 above + 8 MB rows); per row U at +0,
 constexpr int kCV = VP8G_CV;    // V at +kCV, each a ring of two 8-B MB columns
 constexpr bool kC8 = kLfUV % 8 == 0 && kTP % 8 == 0 && kCV % 8 == 0;  // chroma 8-B pieces 8-B aligned
-static_assert(kLfUV >= 20 * kTP && kCV >= 16 && kCV + 16 <= kTP, "tile layout");
-constexpr int kAbY = (kLfUV + 12 * kTP + 15) & ~15;  // luma above row: [15] corner P, [16..31] A, [32..35] above-right
+// V rows may sit rows away from their U rows (kCV >= kTP: V row r shares a physical row with U row
+// r + kCV / kTP, in bytes kCV % kTP ..+16): with kCV = 64 at pitch 40 (V at 24..39 of the next row)
+// the 32 rows a vertical-edge gather touches -- 16 luma, 8 U, 8 V -- fall on 32 distinct banks
+// (tools/lds_banks.py), where U and V side by side (kCV = 16) met two rows per bank.
+static_assert(kLfUV >= 20 * kTP && kCV % kTP >= 16 && kCV % kTP + 16 <= kTP, "tile layout");
+constexpr int kUVBytes = 12 * kTP > kCV + 11 * kTP + 16 ? 12 * kTP : kCV + 11 * kTP + 16;  // chroma tile span
+constexpr int kAbY = (kLfUV + kUVBytes + 15) & ~15;  // luma above row: [15] corner P, [16..31] A, [32..35] above-right
 constexpr int kAbUV = kAbY + 48;   // chroma above rows: U P@7 A@8..15, V P@23 A@24..31
 constexpr int kColY = kAbUV + 32;  // B_PRED: luma columns 11, 7, 3 of the MB (16 B each, in that order),
                                    // so that the left column of sub-block column j is at kLeft - 16 j

@@ -12,6 +12,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
+#include <condition_variable>
 #include <mutex>
 #include <vector>
 
@@ -101,10 +103,11 @@ inline uint64_t mb_count(const Vp8DecodedFrame* d) { return (uint64_t)d->mb_cols
 
 inline uint64_t align256(uint64_t x) { return (x + 255) & ~(uint64_t)255; }
 
-// Device-side state shared by all calls of the process (guarded by a mutex: the reference's
-// entry points are reentrant, so concurrent callers must be safe).
+// Device-side state of one call: its stream, device buffers (grown on demand, kept for the next
+// call) and status word.  The reference's entry points are reentrant, so concurrent callers must be
+// safe: a call leases one of up to kMaxCtx contexts (a pool guarded by a mutex; a caller waits only
+// when every context is in use), so up to kMaxCtx threads decode at once, each on its own stream.
 struct DevState {
-	std::mutex mu;
 	bool ready = false;
 	hipStream_t stream = nullptr;
 	uint8_t* in = nullptr;
@@ -124,7 +127,39 @@ struct DevState {
 	uint32_t epoch = 0;  // launch counter for the snapshot flags
 	uint32_t* status = nullptr;
 };
-DevState g_dev;
+constexpr int kMaxCtx = 8;
+struct DevPool {
+	std::mutex mu;
+	std::condition_variable cv;
+	DevState ctx[kMaxCtx];
+	bool busy[kMaxCtx] = {};
+	std::atomic<int> active{0};  // leased contexts (cross-workgroup launch modes run only when alone)
+};
+DevPool g_pool;
+struct Lease {
+	DevState* d;
+	int i;
+	Lease() {
+		std::unique_lock<std::mutex> lk(g_pool.mu);
+		for (;;) {
+			for (i = 0; i < kMaxCtx && g_pool.busy[i]; i++) {
+			}
+			if (i < kMaxCtx) break;
+			g_pool.cv.wait(lk);
+		}
+		g_pool.busy[i] = true;
+		g_pool.active.fetch_add(1);
+		d = &g_pool.ctx[i];
+	}
+	~Lease() {
+		std::lock_guard<std::mutex> lk(g_pool.mu);
+		g_pool.busy[i] = false;
+		g_pool.active.fetch_sub(1);
+		g_pool.cv.notify_one();
+	}
+	Lease(const Lease&) = delete;
+	Lease& operator=(const Lease&) = delete;
+};
 
 hipError_t grow(uint8_t** p, size_t* cap, size_t need) {
 	if (need <= *cap) return hipSuccess;
@@ -137,13 +172,13 @@ hipError_t grow(uint8_t** p, size_t* cap, size_t need) {
 	return e;
 }
 
-hipError_t dev_init() {
-	if (g_dev.ready) return hipSuccess;
-	hipError_t e = hipStreamCreateWithFlags(&g_dev.stream, hipStreamNonBlocking);
+hipError_t dev_init(DevState& g) {
+	if (g.ready) return hipSuccess;
+	hipError_t e = hipStreamCreateWithFlags(&g.stream, hipStreamNonBlocking);
 	if (e != hipSuccess) return e;
-	e = hipMalloc((void**)&g_dev.status, 256);
+	e = hipMalloc((void**)&g.status, 256);
 	if (e != hipSuccess) return e;
-	g_dev.ready = true;
+	g.ready = true;
 	return hipSuccess;
 }
 
@@ -184,9 +219,12 @@ uint32_t split_env() {
 	return e ? (uint32_t)strtoul(e, nullptr, 10) : 0u;
 }
 
-// Launch over device-resident data (caller holds g_dev.mu).  `may_split`: the call completes
-// (stream synchronised) before g_dev.mu is released, so the shared split-mode buffers are safe.
-int run_locked(const std::vector<Vp8gFrameDesc>& descs, const Vp8gBatchArrays& arr, uint8_t* d_out, hipStream_t s,
+// Launch over device-resident data with the buffers of the leased context g.  `may_split`: the
+// call completes (stream synchronised) before its lease ends.  Launch modes whose workgroups wait on
+// each other across CUs (split parts, the chain's mirror split) need every workgroup of the launch
+// resident: they are chosen only while no other context is leased (a concurrent caller's kernels
+// could otherwise hold the CUs; every such wait is bounded anyway).
+int run_locked(DevState& g_dev, const std::vector<Vp8gFrameDesc>& descs, const Vp8gBatchArrays& arr, uint8_t* d_out, hipStream_t s,
                uint32_t waves_hint, uint8_t* d_descs, bool may_split) {
 	uint32_t max_cols = 0, max_rows = 0;
 	for (const auto& d : descs) {
@@ -199,10 +237,12 @@ int run_locked(const std::vector<Vp8gFrameDesc>& descs, const Vp8gBatchArrays& a
 		if (e) waves_hint = (uint32_t)strtoul(e, nullptr, 10);
 	}
 	const uint32_t env = split_env();
+	const bool alone = g_pool.active.load() <= 1;  // (see above: cross-workgroup waits only when alone)
+	may_split = may_split && alone;
 	// small batches on the host APIs: 8-wave parts, up to kMaxSplit per frame (measured on one 4K
 	// frame: 8 waves x 8 parts 3.9 ms per call, 16 waves x 1..8 parts 8.1..4.7 ms)
 	uint32_t nw = vp8g::pick_waves(waves_hint, max_rows, n);
-	if ((may_split || env > 1) && env != 1 && !waves_hint && vp8g::pick_split(env, n, 8, max_rows) > 1) nw = 8;
+	if ((may_split || (env > 1 && alone)) && env != 1 && !waves_hint && vp8g::pick_split(env, n, 8, max_rows) > 1) nw = 8;
 	uint8_t* gctx = nullptr;
 #ifdef VP8G_FORCE_GCTX  // diagnostic: per-column context in device memory for every frame
 	const bool big = true;
@@ -215,7 +255,7 @@ int run_locked(const std::vector<Vp8gFrameDesc>& descs, const Vp8gBatchArrays& a
 		gctx = g_dev.gctx;
 	}
 	uint32_t k = 1;
-	if (!big && (may_split || env > 1) && env != 1) k = vp8g::pick_split(env, n, nw, max_rows);
+	if (!big && (may_split || (env > 1 && alone)) && env != 1) k = vp8g::pick_split(env, n, nw, max_rows);
 	uint8_t* mbox = nullptr;
 	uint32_t* gprog = nullptr;
 	if (k > 1) {
@@ -230,7 +270,7 @@ int run_locked(const std::vector<Vp8gFrameDesc>& descs, const Vp8gBatchArrays& a
 		const uint32_t wg = vp8g::pick_chain(descs.data(), n, max_cols, &ordered);
 		if (wg) {
 			// mirror split (vp8g_kernels.hip, kSegTop): snapshot buffers and a fresh epoch for the flags
-			const bool split = vp8g::pick_chain_split(n, max_cols, wg, ordered);
+			const bool split = alone && vp8g::pick_chain_split(n, max_cols, wg, ordered);
 			if (split) {
 				HIP_TRY(grow(&g_dev.snap, &g_dev.snap_cap, (size_t)n * max_cols * vp8g::kCtxBytesPerCol), "hipMalloc(snapshots)");
 				const size_t old_cap = g_dev.sflags_cap;
@@ -352,8 +392,8 @@ VP8G_API int vp8g_decode_batch_device(const Vp8gFrameDesc* h_descs, const Vp8gFr
 			return -1;
 		}
 	std::vector<Vp8gFrameDesc> v(h_descs, h_descs + n);
-	std::lock_guard<std::mutex> lk(g_dev.mu);
-	return run_locked(v, *arrays, d_out, (hipStream_t)stream, waves, (uint8_t*)d_descs, false);
+	Lease lease;
+	return run_locked(*lease.d, v, *arrays, d_out, (hipStream_t)stream, waves, (uint8_t*)d_descs, false);
 }
 
 VP8G_API int vp8g_reconstruct_batch(const Vp8KeyFrameHeader* const* kfs, const Vp8DecodedFrame* const* frames, uint32_t n,
@@ -378,7 +418,8 @@ VP8G_API int vp8g_reconstruct_batch(const Vp8KeyFrameHeader* const* kfs, const V
 			return -1;
 		}
 	}
-	std::lock_guard<std::mutex> lk(g_dev.mu);
+	Lease lease;
+	DevState& g_dev = *lease.d;
 	auto fail = [&](void) {
 		for (uint32_t k = 0; k < n; k++) yuv420_free(&outs[k]);
 		errno = EIO;
@@ -392,7 +433,7 @@ VP8G_API int vp8g_reconstruct_batch(const Vp8KeyFrameHeader* const* kfs, const V
 			return fail();            \
 		}                             \
 	} while (0)
-	TRY(dev_init(), "init");
+	TRY(dev_init(g_dev), "init");
 	const InLayout L = in_layout(mbs, 0);
 	TRY(grow(&g_dev.in, &g_dev.in_cap, L.total), "hipMalloc(in)");
 	TRY(grow(&g_dev.out, &g_dev.out_cap, outb ? outb : 256), "hipMalloc(out)");
@@ -428,7 +469,7 @@ VP8G_API int vp8g_reconstruct_batch(const Vp8KeyFrameHeader* const* kfs, const V
 	arr.bmode = in + L.bm;
 	arr.src = nullptr;
 	arr.status = g_dev.status;
-	if (run_locked(descs, arr, g_dev.out, s, 0, g_dev.desc, true) != 0) return fail();
+	if (run_locked(g_dev, descs, arr, g_dev.out, s, 0, g_dev.desc, true) != 0) return fail();
 	for (uint32_t i = 0; i < n; i++) {
 		const Vp8gFrameDesc& d = descs[i];
 		const size_t ysz = (size_t)d.stride_y * d.height, uvsz = (size_t)d.stride_uv * ((d.height + 1) / 2);
@@ -495,8 +536,9 @@ VP8G_API int vp8_loopfilter_apply_keyframe(Yuv420Image* img, const Vp8DecodedFra
 	desc.src_stride_uv = desc.stride_uv;
 	std::vector<Vp8gFrameDesc> descs(1, desc);
 	const uint64_t k = mb_count(d);
-	std::lock_guard<std::mutex> lk(g_dev.mu);
-	HIP_TRY(dev_init(), "init");
+	Lease lease;
+	DevState& g_dev = *lease.d;
+	HIP_TRY(dev_init(g_dev), "init");
 	const InLayout L = in_layout(k, frame_bytes);
 	HIP_TRY(grow(&g_dev.in, &g_dev.in_cap, L.total), "hipMalloc(in)");
 	HIP_TRY(grow(&g_dev.out, &g_dev.out_cap, frame_bytes), "hipMalloc(out)");
@@ -524,7 +566,7 @@ VP8G_API int vp8_loopfilter_apply_keyframe(Yuv420Image* img, const Vp8DecodedFra
 	arr.bmode = nullptr;
 	arr.src = src;
 	arr.status = g_dev.status;
-	if (run_locked(descs, arr, g_dev.out, s, 0, g_dev.desc, true) != 0) return -1;
+	if (run_locked(g_dev, descs, arr, g_dev.out, s, 0, g_dev.desc, true) != 0) return -1;
 	HIP_TRY(hipMemcpy2DAsync(img->y, img->stride_y, g_dev.out, img->width, img->width, img->height, hipMemcpyDeviceToHost, s),
 	        "D2H");
 	HIP_TRY(hipMemcpy2DAsync(img->u, img->stride_uv, g_dev.out + desc.out_u, cw, cw, ch, hipMemcpyDeviceToHost, s), "D2H");
