@@ -126,6 +126,10 @@ struct DevState {
 	size_t sflags_cap = 0;
 	uint32_t epoch = 0;  // launch counter for the snapshot flags
 	uint32_t* status = nullptr;
+	// (device batch API: the call returns before its kernel ends; the next lease of this context
+	// orders its work on the context's buffers after that kernel)
+	hipEvent_t done = nullptr;
+	bool pending = false;
 };
 constexpr int kMaxCtx = 8;
 struct DevPool {
@@ -232,6 +236,10 @@ int run_locked(DevState& g_dev, const std::vector<Vp8gFrameDesc>& descs, const V
 		if (d.mb_rows > max_rows) max_rows = d.mb_rows;
 	}
 	const uint32_t n = (uint32_t)descs.size();
+	if (g_dev.pending) {  // the previous (asynchronous) launch on this context's buffers comes first
+		HIP_TRY(hipStreamWaitEvent(s, g_dev.done, 0), "hipStreamWaitEvent");
+		g_dev.pending = false;
+	}
 	if (!waves_hint) {
 		const char* e = getenv("VP8G_WAVES");  // override of the default waves per workgroup
 		if (e) waves_hint = (uint32_t)strtoul(e, nullptr, 10);
@@ -393,7 +401,12 @@ VP8G_API int vp8g_decode_batch_device(const Vp8gFrameDesc* h_descs, const Vp8gFr
 		}
 	std::vector<Vp8gFrameDesc> v(h_descs, h_descs + n);
 	Lease lease;
-	return run_locked(*lease.d, v, *arrays, d_out, (hipStream_t)stream, waves, (uint8_t*)d_descs, false);
+	DevState& g = *lease.d;
+	if (!g.done) HIP_TRY(hipEventCreateWithFlags(&g.done, hipEventDisableTiming), "hipEventCreate");
+	if (run_locked(g, v, *arrays, d_out, (hipStream_t)stream, waves, (uint8_t*)d_descs, false) != 0) return -1;
+	HIP_TRY(hipEventRecord(g.done, (hipStream_t)stream), "hipEventRecord");
+	g.pending = true;
+	return 0;
 }
 
 VP8G_API int vp8g_reconstruct_batch(const Vp8KeyFrameHeader* const* kfs, const Vp8DecodedFrame* const* frames, uint32_t n,
