@@ -59,7 +59,11 @@ constexpr int kDqTable = kBpTable + kBpModes * 16 * kBpEntry;  // 4 segments x 6
 constexpr int kLfTable = kDqTable + 48;                 // 4 segments x 2 (B_PRED?) x {E, I, T, 0}
 constexpr int kTabStride = 80;                          // per frame slot (chain mode: two slots)
 constexpr int kMisc = kDqTable + 2 * kTabStride;        // chain mode: list length
-constexpr int kHdrBytes = kMisc + 16;
+#ifndef VP8G_PRED_ROLE  // whole-block predictor: lane roles from a per-lane LDS word pair (kRoleTab)
+#define VP8G_PRED_ROLE 1
+#endif
+constexpr int kRoleTab = kMisc + 16;                    // (VP8G_PRED_ROLE) 32 lanes x 8 B
+constexpr int kHdrBytes = kRoleTab + (VP8G_PRED_ROLE ? 256 : 0);
 
 // Shared per-MB-column context (one frame per workgroup).
 constexpr int kCtxRecBytes = 32;   // unfiltered bottom row: Y 16, U 8, V 8 (intra prediction)

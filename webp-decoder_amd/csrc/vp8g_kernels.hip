@@ -229,6 +229,34 @@ constexpr BorderTab make_bordertab() {
 }
 __constant__ BorderTab kBorderTab = make_bordertab();
 
+// Whole-block predictor roles of lanes 0..23 (VP8G_PRED_ROLE; offsets from the half's area):
+// v[2 ln] = above-row base | own above word << 11 | is-luma << 22 | last block row << 23 | last
+// block column << 24 | offset in the ctx_rec column << 25; v[2 ln + 1] = left-column base |
+// destination in the tile at slot 0 << 11 | block row << 22.
+struct PredRoleTab {
+	uint32_t v[64];
+};
+constexpr PredRoleTab make_predroletab() {
+	PredRoleTab t{};
+	for (int ln = 0; ln < 24; ln++) {
+		const bool yl = ln < 16;
+		const int p = yl ? 0 : (ln - 16) >> 2;
+		const int blk = yl ? ln : (ln & 3);
+		const int bx = yl ? (blk & 3) : (blk & 1), by = yl ? (blk >> 2) : (blk >> 1);
+		const int ab = yl ? kAbY + 16 : kAbUV + 16 * p + 8;
+		const int lc = yl ? kLeft : kLeft + 16 + 8 * p;
+		const int dst = yl ? kLfY + (4 + 4 * by) * kTP + 4 * bx : kLfUV + p * kCV + (4 + 4 * by) * kTP + 4 * bx;
+		const int rec = yl ? 4 * bx : 16 + 8 * p + 4 * bx;
+		const int last = yl ? 3 : 1;
+		t.v[2 * ln] = (uint32_t)ab | ((uint32_t)(ab + 4 * bx) << 11) | ((yl ? 1u : 0u) << 22) | ((by == last ? 1u : 0u) << 23) |
+		              ((bx == last ? 1u : 0u) << 24) | ((uint32_t)rec << 25);
+		t.v[2 * ln + 1] = (uint32_t)lc | ((uint32_t)dst << 11) | ((uint32_t)by << 22);
+	}
+	return t;
+}
+__constant__ PredRoleTab kPredRoleTab = make_predroletab();
+static_assert(kLeft + 32 < 2048 && kAbUV + 40 < 2048 && kLfUV + kCV + 20 * kTP < 2048, "11-bit role offsets");
+
 
 // ---------------------------------------------------------------------------------------------
 // small helpers
@@ -763,6 +791,9 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 	const uint32_t part = kS ? blockIdx.x / nfr : 0u;
 
 	for (int i = (int)threadIdx.x; i < kBpModes * 16 * (kBpEntry / 4); i += NW * 64) ((uint32_t*)(smem + kBpTable))[i] = kBpTab.v[i];
+#if VP8G_PRED_ROLE
+	if (threadIdx.x < 64) ((uint32_t*)(smem + kRoleTab))[threadIdx.x] = kPredRoleTab.v[threadIdx.x];
+#endif
 	uint32_t bt_l = kBorderTab.v[lane0 & 31];  // this lane's border-setup role (loop-invariant)
 	// dequant / loop-filter tables of a frame into its slot (chain mode: by the wave of the frame's pair 0)
 	auto put_tables = [&](const Vp8gFrameDesc& Df, uint32_t tabo, int l) {
@@ -1279,6 +1310,9 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 
 			// ---------------------------------------------- borders + loop-filter top strip
 			PRIO(2);
+#if VP8G_PRED_ROLE
+			const u32x2 prole = ld64(smem + kRoleTab + 8 * ln);  // (used by the predictor; rides the border loads' round trip)
+#endif
 			if (act) {
 				const bool top = r == 0;
 				if (lf_only) {
@@ -1341,12 +1375,18 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 					// whole-block predictors (RFC 12.2; reference vp8_recon.c:152-212, 533-560, 605-651),
 					// one 4x4 block per lane, branch-free: every mode is sat8(L' + A' + K) with
 					// L' = L & mL, A' = A & mA (DC: K = dc value; V: mA; H: mL; TM: both, K = -P)
+#if VP8G_PRED_ROLE
+					const bool yl = (prole.x >> 22) & 1u;
+					const uint8_t* ab = hv + (prole.x & 0x7FFu);
+					const uint8_t* lc = hv + (prole.y & 0x7FFu);
+#else
 					const bool yl = ln < 16;
 					const int p = (ln - 16) >> 2;  // chroma plane (chroma lanes)
 					const int blk = yl ? ln : (ln & 3);
 					const int bx = yl ? (blk & 3) : (blk & 1), by = yl ? (blk >> 2) : (blk >> 1);
 					const uint8_t* ab = yl ? abY + 16 : abUV + 16 * p + 8;
 					const uint8_t* lc = yl ? left : left + 16 + 8 * p;
+#endif
 					const int mode = yl ? (ymode > 4 ? 0 : ymode) : (uvmode > 3 ? 0 : uvmode);
 					const u32x2 a01 = ld64(ab), a23 = ld64(ab + 8), l01 = ld64(lc), l23 = ld64(lc + 8);
 					const uint32_t sa2 = __builtin_amdgcn_sad_u8(a01.y, 0u, __builtin_amdgcn_sad_u8(a01.x, 0u, 0u));
@@ -1357,16 +1397,25 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 					const uint32_t sum = (ha ? (yl ? sa4 : sa2) : 0u) + (hl ? (yl ? sl4 : sl2) : 0u);
 					const int shift = (yl ? 3 : 2) + (ha ? 1 : 0) + (hl ? 1 : 0);  // 16 or 8 samples per edge
 					const int dcv = (ha || hl) ? (int)((sum + (1u << (shift - 1))) >> shift) : 128;
+#if VP8G_PRED_ROLE
+					const uint32_t aw = ld32(hv + __builtin_amdgcn_ubfe(prole.x, 11u, 11u));
+					const uint32_t lw = ld32(lc + 4u * __builtin_amdgcn_ubfe(prole.y, 22u, 2u));
+#else
 					const uint32_t aw = ld32(ab + 4 * bx);
 					const uint32_t lw = ld32(lc + 4 * by);
+#endif
 					const int P = (int)ab[-1];
 					// two pixels per op as int16 pairs (|residual| < 2^14, so nothing wraps)
 					const uint32_t mA = (mode == 1 || mode == 3) ? 0x00FF00FFu : 0u;
 					const uint32_t mL = (mode == 2 || mode == 3) ? 0x00FF00FFu : 0u;
 					const int K = (mode == 3 ? -P : 0) + (mode == 0 ? dcv : 0);
 					const uint32_t K2 = __builtin_amdgcn_perm((uint32_t)K, (uint32_t)K, 0x05040100u);  // K in both halves
+#if VP8G_PRED_ROLE
+					uint8_t* dst = hv + __builtin_amdgcn_ubfe(prole.y, 11u, 11u) + (slot ? (yl ? 16u : 8u) : 0u);
+#else
 					uint8_t* dst = yl ? tY + (4 + 4 * by) * kTP + slot * 16 + 4 * bx
 					                  : tC + p * kCV + (4 + 4 * by) * kTP + slot * 8 + 4 * bx;
+#endif
 					const uint32_t* const rw = rs;  // this lane's own block
 					const uint32_t A01 = pk_add(__builtin_amdgcn_perm(aw, aw, 0x0C010C00u) & mA, K2);
 					const uint32_t A23 = pk_add(__builtin_amdgcn_perm(aw, aw, 0x0C030C02u) & mA, K2);
@@ -1394,6 +1443,14 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 					for (int rr = 0; rr < 4; rr++) st32(dst + rr * kTP, wv[rr]);
 					// the MB's unfiltered bottom row -> ctx_rec[c] (the next MB row's above row) and its
 					// right column -> the left column of the next MB (reference vp8_recon.c:395-421)
+#if VP8G_PRED_ROLE
+					if ((prole.x >> 23) & 1u) ctx.wr32(rec_off(cu) + (prole.x >> 25), wv[3]);
+					if ((prole.x >> 24) & 1u) {
+						const uint32_t c01 = __builtin_amdgcn_perm(wv[1], wv[0], 0x0C0C0703u);
+						const uint32_t c23 = __builtin_amdgcn_perm(wv[3], wv[2], 0x0C0C0703u);
+						st32(const_cast<uint8_t*>(lc) + 4u * __builtin_amdgcn_ubfe(prole.y, 22u, 2u), __builtin_amdgcn_perm(c23, c01, 0x05040100u));
+					}
+#else
 					const int last = yl ? 3 : 1;
 					if (by == last) ctx.wr32(rec_off(cu) + (yl ? 4 * bx : 16 + 8 * p + 4 * bx), wv[3]);
 					if (bx == last) {
@@ -1401,6 +1458,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 						const uint32_t c23 = __builtin_amdgcn_perm(wv[3], wv[2], 0x0C0C0703u);
 						st32((yl ? left : left + 16 + 8 * p) + 4 * by, __builtin_amdgcn_perm(c23, c01, 0x05040100u));
 					}
+#endif
 				}
 				wave_lds_sync();
 				SUBMARK(20);
