@@ -1115,7 +1115,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 			uint8_t* const tY = hv + kLfY;
 			uint8_t* const tC = hv + kLfUV;  // chroma: U at +0, V at +kCV, row pitch kTP
 			uint8_t* const abY = hv + kAbY;
-			uint8_t* const abUV = hv + kAbUV;
+			[[maybe_unused]] uint8_t* const abUV = hv + kAbUV;  // (the predictor role word carries it)
 			uint8_t* const left = hv + kLeft;
 
 			// per-half side info (lanes 26..29 / 58..61 hold it)
