@@ -4,6 +4,11 @@ reference decoder's own I420 (tests/golden/digests.json).
 
 * 260 x 4K (> 256 CUs: the timed chain kernel `frame_kernel<16, false, false, true>` with the
   mirror split, two frames per workgroup at most);
+* 512 x 4K: the exact uhd4 launch bench.py times (rank 0's shard of BASELINE configs[3] / [4]);
+* 128 synthetic 4K frames of a far shard (global indices 3584..3711: rank 7 of configs[4]);
+* two threads on two streams issuing 300-frame 4K batches back to back while a third calls the
+  single-frame drop-in entry point: the process-wide launch gate (vp8g_device.h, GateScope) keeps
+  the cross-workgroup launch modes from running beside another launch;
 * 1100 x 1080p (the fhd4 workload's geometry);
 * 300 mixed 4K / 1080p frames in a scrambled order (the cost-balanced launch order);
 * 64 distinct synthetic 4K frames of the bench's synthetic batch (seed 0x5EED ^ i);
@@ -226,3 +231,89 @@ def test_chain_mirror_split_forced(vp8g):
                        timeout=240, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout.strip().endswith("OK"), r.stdout
+
+
+def test_device_batch_512_uhd_bench_launch(vp8g, digests):
+    """Verdict r03 #3: the launch bench.py times for uhd4 (512 x 4K, slot i <- fixture i % 4, rank
+    0's shard of BASELINE configs[3] / [4]): the chain kernel with the mirror split, every slot."""
+    b, bad = run_batch(vp8g, UHD, 512, True, digests, slot0=0)
+    assert not bad, f"{len(bad)} of 512 slots differ, e.g. {bad[:8]}"
+    del b
+    torch.cuda.empty_cache()
+
+
+def test_device_batch_synthetic_far_shard(vp8g, digests):
+    """Verdict r03 #3: frames no other test decodes on hardware -- global indices 3584..3711 of the
+    synthetic batch (seed 0x5EED ^ i; rank 7's shard of BASELINE configs[4]), against the digests of
+    the reference decoder's own output (tests/golden/make_digests.py)."""
+    import concurrent.futures as cf
+    import vp8g_batch
+    s = digests["synth_uhd"]
+    lo, hi = 3584, 3712
+    assert len(s["yuvf"]) >= hi
+    n = hi - lo
+    b = vp8g_batch.DeviceBatch(n, s["width"], s["height"], torch.device("cuda:0"))
+    with cf.ThreadPoolExecutor(8) as ex:
+        for i, f in enumerate(ex.map(lambda g: vp8g.synth_frame(s["width"], s["height"], 0x5EED ^ g, s["profile"]), range(lo, hi))):
+            b.fill(i, f, True)
+            f.free()
+    b.commit()
+    stream = torch.cuda.current_stream().cuda_stream
+    b.launch(stream)
+    got = b.digests(stream)
+    assert b.status_word() == 0
+    assert [("0x%016x" % int(d)) for d in got] == s["yuvf"][lo:hi]
+    del b
+    torch.cuda.empty_cache()
+
+
+def test_device_batches_two_streams_and_dropin_concurrently(vp8g, digests):
+    """Verdict r03 #2 / ADVICE r03 (medium): vp8g_decode_batch_device returns before its kernel ends,
+    so two callers on two streams can have launches in flight at once.  300 x 4K per caller takes the
+    chain's mirror split when alone (bottom segments wait on another workgroup's top segment); two
+    such launches side by side, or one beside another kernel, could leave workgroups spinning on
+    partners that cannot get a CU.  Two threads issue four launches each on their own streams while
+    the main thread makes single-frame drop-in calls (whose split mode waits across workgroups too):
+    every status word must stay 0 and every slot and drop-in output must match the reference."""
+    import threading
+    import vp8g_batch
+    dev = torch.device("cuda:0")
+    frames = [vp8g.decode_file(FIXTURES / r) for r in UHD]
+    batches, streams = [], []
+    for t in range(2):
+        b = vp8g_batch.DeviceBatch(300, 3840, 2160, dev)
+        b.replicate(frames, True, slot0=1 + t)
+        b.commit()
+        batches.append(b)
+        streams.append(torch.cuda.Stream(dev))
+    torch.cuda.synchronize()
+    errs = []
+
+    def worker(b, st):
+        try:
+            for _ in range(4):
+                b.launch(st.cuda_stream)
+        except Exception as e:  # noqa: BLE001 (reported below)
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(b, st)) for b, st in zip(batches, streams)]
+    for t in th:
+        t.start()
+    dropins = [vp8g.gpu_reconstruct(frames[i % 4], True) for i in range(3)]
+    for t in th:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in th)
+    torch.cuda.synchronize()
+    assert not errs, errs
+    for t, b in enumerate(batches):
+        assert b.status_word() == 0, f"batch {t}: status 0x{b.status_word():x}"
+        got = b.digests(streams[t].cuda_stream)
+        exp = [int(digests["fixtures"][UHD[(1 + t + i) % 4]]["yuvf"], 16) for i in range(300)]
+        bad = [i for i in range(300) if int(got[i]) != exp[i]]
+        assert not bad, f"batch {t}: {len(bad)} of 300 slots differ, e.g. {bad[:8]}"
+    for i, out in enumerate(dropins):
+        assert vp8g.digest64(out) == int(digests["fixtures"][UHD[i % 4]]["yuvf"], 16), i
+    for f in frames:
+        f.free()
+    del batches
+    torch.cuda.empty_cache()

@@ -105,6 +105,37 @@ inline size_t chain_lds_bytes(uint32_t ctx_cols, uint32_t list_max) {
 	return (size_t)kHdrBytes + (size_t)kChainWaves * kWaveBytes + 2 * (size_t)ctx_cols * kCtxBytesPerCol + 4 * (size_t)list_max;
 }
 
+// Process-wide launch gate (vp8g_shim.hip).  Launch modes whose workgroups wait on each other across
+// CUs -- split parts (launch_frames with nsplit > 1) and the chain's mirror split -- need every
+// workgroup of the launch resident at once.  Beside another kernel of this library (an earlier
+// asynchronous batch on another stream, a pipeline chunk, a device-m05 or writer kernel) some of
+// them could wait for CUs that the others hold while they spin; two such launches side by side
+// would both run into the bounded wait and fail with VP8G_ERR_TIMEOUT.  So every kernel launch of
+// the library is enqueued inside a GateScope, which holds one process-wide mutex from the decision
+// to the last enqueue:
+//   * the scope's stream is first ordered after a cross-workgroup launch still in flight on
+//     another stream (hipStreamWaitEvent), so nothing starts beside one;
+//   * may_cross() is true only when no launch of the library is in flight on any other stream
+//     (hipEventQuery of each stream's last recorded launch), so a cross-workgroup launch never
+//     starts beside another kernel;
+//   * done(crossed) records the launch's completion event for the next caller.
+// Kernels launched by the caller's own code on other streams are outside the gate.
+class GateScope {
+   public:
+	explicit GateScope(hipStream_t s);
+	~GateScope();
+	GateScope(const GateScope&) = delete;
+	GateScope& operator=(const GateScope&) = delete;
+	hipError_t status() const { return err_; }
+	bool may_cross() const { return may_cross_; }
+	hipError_t done(bool crossed);
+
+   private:
+	hipStream_t s_;
+	hipError_t err_ = hipSuccess;
+	bool may_cross_ = false;
+};
+
 // Launch the fused recon(+LF) kernel.  `global_ctx` != nullptr selects the variant whose
 // per-column context lives in device memory (frames too wide for LDS); it must hold
 // n_frames * ctx_cols * kCtxBytesPerCol bytes.

@@ -103,13 +103,16 @@ VP8G_API int vp8g_frame_digests(const Vp8gFrameDesc* h_descs, const Vp8gFrameDes
 		if (len > max_len) max_len = len;
 	}
 	hipStream_t s = (hipStream_t)stream;
-	hipError_t e = hipMemsetAsync(d_digests, 0, (size_t)n * 8, s);
+	vp8g::GateScope gate(s);  // (vp8g_device.h: no cross-workgroup launch beside it)
+	hipError_t e = gate.status();
+	if (e == hipSuccess) e = hipMemsetAsync(d_digests, 0, (size_t)n * 8, s);
 	if (e == hipSuccess) {
 		const uint32_t chunks = (uint32_t)((max_len + kChunk - 1) / kChunk);
 		hipLaunchKernelGGL(digest_kernel, dim3(chunks, n), dim3(kThreads), 0, s, d_descs, d_out,
 		                   (unsigned long long*)d_digests);
 		e = hipGetLastError();
 	}
+	if (e == hipSuccess) e = gate.done(false);
 	if (e != hipSuccess) {
 		vp8g::set_error_text("digest", e);
 		errno = EIO;

@@ -359,8 +359,11 @@ DEV Rsrc plane_rsrc(uint8_t* base, uint32_t bytes) {
 	                    (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
 	return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)bu, (short)0, __builtin_amdgcn_readfirstlane((int)bytes), 0x00020000);
 }
-DEV void bst128(Rsrc r, uint32_t off, u32x4 v) { __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, 0); }
-DEV void bst64(Rsrc r, uint32_t off, u32x2 v) { __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)off, 0, 0); }
+#ifndef VP8G_STORE_AUX  // cache-policy bits of the output pixel stores (A/B experiments)
+#define VP8G_STORE_AUX 0
+#endif
+DEV void bst128(Rsrc r, uint32_t off, u32x4 v) { __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, VP8G_STORE_AUX); }
+DEV void bst64(Rsrc r, uint32_t off, u32x2 v) { __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)off, 0, VP8G_STORE_AUX); }
 
 // single-byte LDS access that the load/store vectoriser leaves alone
 DEV int ldb(const uint8_t* p) { return (int)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT); }
@@ -613,8 +616,11 @@ struct Pref {
 // Occupancy target: two workgroups (frames) per CU at NW <= 8 (2*NW waves per CU); one
 // workgroup of 12 or 16 waves per CU for batches smaller than the CU count (pick_waves).  Either
 // way at most 4 waves per SIMD, i.e. the full 128-VGPR budget.
+#ifndef VP8G_WPS8  // (experiments: waves per SIMD the 8-wave kernel is compiled for -- 6 = 80 VGPRs, three frames per CU)
+#define VP8G_WPS8 4
+#endif
 template <int NW>
-constexpr int min_waves_per_simd() { return NW == 10 ? 5 : (NW >= 6 ? 4 : (NW >= 2 ? (2 * NW) / 4 : 1)); }
+constexpr int min_waves_per_simd() { return NW == 10 ? 5 : (NW == 8 ? VP8G_WPS8 : (NW >= 6 ? 4 : (NW >= 2 ? (2 * NW) / 4 : 1))); }
 
 // Split mode (kS, small batches): a frame's MB row pairs are dealt over `nsplit` workgroups
 // ("parts") of NW waves each -- global wave g = part * NW + wave owns pairs g, g + nsplit*NW, ...
@@ -1787,6 +1793,16 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 #endif
 }
 
+// The dynamic-LDS limit of a kernel instantiation, set once to the whole of the CU's LDS (the
+// kernel has no static LDS): concurrent launches from several threads then never race a smaller
+// value set by another thread between its own set and launch.
+template <int NW, bool kG, bool kS, bool kC>
+hipError_t lds_attr() {
+	static const hipError_t e =
+	    hipFuncSetAttribute((const void*)frame_kernel<NW, kG, kS, kC>, hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLds);
+	return e;
+}
+
 template <int NW, bool kG, bool kS>
 hipError_t launch_t(const Vp8gFrameDesc* d_descs, uint32_t n, const Vp8gBatchArrays& arrays, uint8_t* d_out,
                     uint32_t ctx_cols, uint8_t* gctx, uint32_t nsplit, uint8_t* mbox, uint32_t* gprog, hipStream_t stream,
@@ -1794,7 +1810,7 @@ hipError_t launch_t(const Vp8gFrameDesc* d_descs, uint32_t n, const Vp8gBatchArr
 	const size_t lds = lds_bytes(NW, ctx_cols, kG);
 	auto fn = frame_kernel<NW, kG, kS, false>;
 	if (lds > 65536) {
-		hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+		hipError_t e = lds_attr<NW, kG, kS, false>();
 		if (e != hipSuccess) return e;
 	}
 	hipLaunchKernelGGL(fn, dim3(n * (kS ? nsplit : 1u)), dim3(NW * 64), lds, stream, d_descs, arrays, d_out, ctx_cols, gctx,
@@ -1923,7 +1939,7 @@ hipError_t launch_chain(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const V
 	const uint32_t list_max = (n_frames + workgroups - 1) / workgroups;
 	const size_t lds = chain_lds_bytes(ctx_cols, split ? 2 * list_max : list_max);
 	auto fn = frame_kernel<kChainWaves, false, false, true>;
-	hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+	hipError_t e = lds_attr<kChainWaves, false, false, true>();
 	if (e != hipSuccess) return e;
 	// (chain kernel arguments: gctx = snapshots, gprog = flags, nsplit = epoch, ord_first = ordered | split << 1)
 	hipLaunchKernelGGL(fn, dim3(workgroups), dim3(kChainWaves * 64), lds, stream, d_descs, arrays, d_out, ctx_cols,

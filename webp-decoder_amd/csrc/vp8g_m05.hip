@@ -482,9 +482,17 @@ VP8G_API int vp8g_m05_batch_device(const Vp8gTokFrame* h_jobs, const Vp8gTokFram
 	o.hasc = const_cast<uint8_t*>(arrays->has_coeff);
 	o.bmode = const_cast<uint8_t*>(arrays->bmode);
 	o.status = arrays->status;
-	hipLaunchKernelGGL(m05_kernel, dim3(n), dim3(64u * (1u + max_parts)), (kCtlWords + kRing / 4u + 2u * max_cols) * 4u,
-	                   (hipStream_t)hip_stream, d_jobs, d_bits, o);
-	const hipError_t e = hipGetLastError();
+	hipError_t e;
+	{
+		vp8g::GateScope gate((hipStream_t)hip_stream);  // (vp8g_device.h: no cross-workgroup launch beside it)
+		e = gate.status();
+		if (e == hipSuccess) {
+			hipLaunchKernelGGL(m05_kernel, dim3(n), dim3(64u * (1u + max_parts)), (kCtlWords + kRing / 4u + 2u * max_cols) * 4u,
+			                   (hipStream_t)hip_stream, d_jobs, d_bits, o);
+			e = hipGetLastError();
+		}
+		if (e == hipSuccess) e = gate.done(false);
+	}
 	if (e != hipSuccess) {
 		vp8g::set_error_text("m05 launch", e);
 		errno = EIO;

@@ -565,7 +565,7 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 			uint32_t nw = vp8g::pick_waves(0, max_rows, nf);
 			if (alone && vp8g::pick_split(0, nf, 8, max_rows) > 1) nw = 8;
 			const bool big = vp8g::lds_bytes((int)nw, max_cols, false) > (size_t)vp8g::kMaxLds;
-			const uint32_t k = big || !alone ? 1u : vp8g::pick_split(0, nf, nw, max_rows);
+			const uint32_t k_plan = big || !alone ? 1u : vp8g::pick_split(0, nf, nw, max_rows);
 			ChunkLayout L;
 			uint64_t o = 0;
 			L.ym = o, o = al256(o + mbs);
@@ -585,8 +585,8 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 			L.desc = o, o = al256(o + nf * sizeof(Vp8gFrameDesc));
 			L.status = o, o = al256(o + 4);
 			L.gctx = o, o = al256(o + (big ? (uint64_t)nf * max_cols * vp8g::kCtxBytesPerCol : 0));
-			L.mbox = o, o = al256(o + (k > 1 ? (uint64_t)nf * k * max_cols * vp8g::kCtxBytesPerCol : 0));
-			L.gprog = o, o = al256(o + (k > 1 ? (uint64_t)nf * k * 4 : 0));
+			L.mbox = o, o = al256(o + (k_plan > 1 ? (uint64_t)nf * k_plan * max_cols * vp8g::kCtxBytesPerCol : 0));
+			L.gprog = o, o = al256(o + (k_plan > 1 ? (uint64_t)nf * k_plan * 4 : 0));
 			L.out = o, o = al256(o + outb);
 			L.total = o;
 			const double tg = trace ? ms_now() : 0.0;
@@ -648,9 +648,13 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 				        nf, (unsigned long long)mbs, ms_now());
 			PTRY(hipMemcpyAsync(d + L.desc, s.descs.data(), nf * sizeof(Vp8gFrameDesc), hipMemcpyHostToDevice, stream), "H2D");
 			PTRY(hipMemsetAsync(d + L.status, 0, 4, stream), "memset");
-			if (k > 1) PTRY(hipMemsetAsync(d + L.gprog, 0, (size_t)nf * k * 4, stream), "memset");
-			// -- expansion (or device m05) + recon(+LF)
+			// -- expansion (or device m05) + recon(+LF), inside the process-wide launch gate
+			// (vp8g_device.h): the split mode only when no other launch of the library is in flight
 			{
+				vp8g::GateScope gate(stream);
+				PTRY(gate.status(), "hipStreamWaitEvent(gate)");
+				const uint32_t k = k_plan > 1 && gate.may_cross() ? k_plan : 1u;
+				if (k > 1) PTRY(hipMemsetAsync(d + L.gprog, 0, (size_t)nf * k * 4, stream), "memset");
 				Vp8gBatchArrays arr;
 				arr.coeff_y = (const int16_t*)(d + L.cy);
 				arr.coeff_u = (const int16_t*)(d + L.cu);
@@ -689,6 +693,7 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 					                         big ? d + L.gctx : nullptr, stream, nw, k, k > 1 ? d + L.mbox : nullptr,
 					                         k > 1 ? (uint32_t*)(d + L.gprog) : nullptr),
 					     "recon launch");
+				PTRY(gate.done(k > 1), "hipEventRecord(gate)");
 			}
 			// -- D2H into the callers' images, by this kind's Copier once the kernels are done
 			PTRY(hipEventRecord(s.kdone, stream), "event");

@@ -665,14 +665,15 @@ VP8G_API int vp8g_encode_batch_device(const Vp8gEncDesc* h, const Vp8gEncDesc* d
 	}
 	uint32_t* tab = nullptr;
 	const int cus = vp8g::device_cus();
-	hipError_t e = hipSuccess;
-	{
+	hipError_t e = any_png ? tables_dev(&tab) : hipSuccess;
+	vp8g::GateScope gate((hipStream_t)stream);  // (vp8g_device.h: no cross-workgroup launch beside these)
+	if (e == hipSuccess) e = gate.status();
+	if (e == hipSuccess) {
 		const uint32_t grid = min(total, (uint32_t)(cus > 0 ? cus : 256) * 16u);
 		hipLaunchKernelGGL(enc_write_kernel, dim3(grid), dim3(kPlainThreads), 0, (hipStream_t)stream, d_descs, n, total, d_src,
 		                   d_out);
 		e = hipGetLastError();
 	}
-	if (e == hipSuccess && any_png) e = tables_dev(&tab);
 	if (e == hipSuccess && any_png) {
 		const uint32_t grid = min(total, (uint32_t)(cus > 0 ? cus : 256) * 4u);
 		hipLaunchKernelGGL(crc_kernel, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, d_descs, n, total, d_out,
@@ -684,6 +685,7 @@ VP8G_API int vp8g_encode_batch_device(const Vp8gEncDesc* h, const Vp8gEncDesc* d
 		                   d_out, tab);
 		e = hipGetLastError();
 	}
+	if (e == hipSuccess) e = gate.done(false);
 	if (e != hipSuccess) {
 		vp8g::set_error_text("encode launch", e);
 		errno = EIO;

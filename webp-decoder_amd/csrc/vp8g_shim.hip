@@ -137,7 +137,6 @@ struct DevPool {
 	std::condition_variable cv;
 	DevState ctx[kMaxCtx];
 	bool busy[kMaxCtx] = {};
-	std::atomic<int> active{0};  // leased contexts (cross-workgroup launch modes run only when alone)
 };
 DevPool g_pool;
 struct Lease {
@@ -152,27 +151,129 @@ struct Lease {
 			g_pool.cv.wait(lk);
 		}
 		g_pool.busy[i] = true;
-		g_pool.active.fetch_add(1);
 		d = &g_pool.ctx[i];
 	}
 	~Lease() {
 		std::lock_guard<std::mutex> lk(g_pool.mu);
 		g_pool.busy[i] = false;
-		g_pool.active.fetch_sub(1);
 		g_pool.cv.notify_one();
 	}
 	Lease(const Lease&) = delete;
 	Lease& operator=(const Lease&) = delete;
 };
 
-hipError_t grow(uint8_t** p, size_t* cap, size_t need) {
+// The process-wide launch gate (vp8g_device.h, GateScope): each stream's last launch of the library
+// and the last cross-workgroup launch, as events.
+struct GateEntry {
+	hipStream_t s;
+	hipEvent_t ev;
+	bool live;
+};
+struct Gate {
+	std::recursive_mutex mu;  // (the pipeline's chunk scope encloses vp8g_m05_batch_device's own)
+	std::vector<GateEntry> last;
+	hipEvent_t xev = nullptr;
+	hipStream_t xs = nullptr;
+	bool xpending = false;
+};
+Gate g_gate;
+
+// Device memory held by all contexts (the buffers below), so that concurrent large callers do not
+// accumulate eight working sets: growing past half of the device's memory first releases the buffers
+// of idle contexts.
+std::atomic<size_t> g_held{0};
+
+
+}  // namespace
+
+vp8g::GateScope::GateScope(hipStream_t s) : s_(s) {
+	g_gate.mu.lock();
+	if (g_gate.xpending) {
+		const hipError_t q = hipEventQuery(g_gate.xev);
+		if (q == hipSuccess) g_gate.xpending = false;
+		else if (g_gate.xs != s) err_ = hipStreamWaitEvent(s, g_gate.xev, 0);
+	}
+	may_cross_ = !g_gate.xpending || g_gate.xs == s;
+	for (GateEntry& x : g_gate.last) {
+		if (!x.live || x.s == s) continue;
+		if (hipEventQuery(x.ev) == hipSuccess) x.live = false;
+		else may_cross_ = false;  // in flight (or unknown): no cross-workgroup launch beside it
+	}
+	(void)hipGetLastError();  // (hipErrorNotReady of the queries must not read as a launch failure later)
+}
+
+vp8g::GateScope::~GateScope() { g_gate.mu.unlock(); }
+
+hipError_t vp8g::GateScope::done(bool crossed) {
+	GateEntry* slot = nullptr;
+	for (GateEntry& x : g_gate.last)
+		if (x.s == s_ || (!slot && !x.live)) slot = &x;
+	if (!slot) {
+		GateEntry x{s_, nullptr, false};
+		hipError_t e = hipEventCreateWithFlags(&x.ev, hipEventDisableTiming);
+		if (e != hipSuccess) return e;
+		g_gate.last.push_back(x);
+		slot = &g_gate.last.back();
+	}
+	slot->s = s_;
+	hipError_t e = hipEventRecord(slot->ev, s_);
+	if (e != hipSuccess) return e;
+	slot->live = true;
+	if (crossed) {
+		if (!g_gate.xev && (e = hipEventCreateWithFlags(&g_gate.xev, hipEventDisableTiming)) != hipSuccess) return e;
+		if ((e = hipEventRecord(g_gate.xev, s_)) != hipSuccess) return e;
+		g_gate.xs = s_;
+		g_gate.xpending = true;
+	}
+	return hipSuccess;
+}
+
+namespace {
+
+// Grow a buffer of context g.  The context's last asynchronous launch (device batch API) may still
+// read its buffers: it completes before one is freed.  Past half of the device's memory held by all
+// contexts, the idle contexts' buffers are released first.
+hipError_t grow(DevState& g, uint8_t** p, size_t* cap, size_t need);
+void release_buffers(DevState& g) {
+	uint8_t** const bufs[] = {&g.in, &g.out, &g.desc, &g.gctx, &g.mbox, &g.snap, &g.sflags};
+	size_t* const caps[] = {&g.in_cap, &g.out_cap, &g.desc_cap, &g.gctx_cap, &g.mbox_cap, &g.snap_cap, &g.sflags_cap};
+	for (int i = 0; i < 7; i++) {
+		if (*bufs[i]) (void)hipFree(*bufs[i]);
+		*bufs[i] = nullptr;
+		g_held.fetch_sub(*caps[i]);
+		*caps[i] = 0;
+	}
+}
+void trim_idle(const DevState* keep) {
+	std::lock_guard<std::mutex> lk(g_pool.mu);
+	for (int i = 0; i < kMaxCtx; i++) {
+		DevState& o = g_pool.ctx[i];
+		if (g_pool.busy[i] || &o == keep || !o.ready) continue;
+		if (o.pending) {
+			if (hipEventSynchronize(o.done) != hipSuccess) continue;
+			o.pending = false;
+		}
+		release_buffers(o);
+	}
+}
+hipError_t grow(DevState& g, uint8_t** p, size_t* cap, size_t need) {
 	if (need <= *cap) return hipSuccess;
+	if (g.pending) {
+		hipError_t e = hipEventSynchronize(g.done);
+		if (e != hipSuccess) return e;
+	}
 	if (*p) (void)hipFree(*p);
+	g_held.fetch_sub(*cap);
 	*p = nullptr;
 	*cap = 0;
-	size_t n = need + need / 4;
+	const size_t n = need + need / 4;
+	size_t fr = 0, tot = 0;
+	if (hipMemGetInfo(&fr, &tot) == hipSuccess && g_held.load() + n > tot / 2) trim_idle(&g);
 	hipError_t e = hipMalloc((void**)p, n);
-	if (e == hipSuccess) *cap = n;
+	if (e == hipSuccess) {
+		*cap = n;
+		g_held.fetch_add(n);
+	}
 	return e;
 }
 
@@ -226,8 +327,8 @@ uint32_t split_env() {
 // Launch over device-resident data with the buffers of the leased context g.  `may_split`: the
 // call completes (stream synchronised) before its lease ends.  Launch modes whose workgroups wait on
 // each other across CUs (split parts, the chain's mirror split) need every workgroup of the launch
-// resident: they are chosen only while no other context is leased (a concurrent caller's kernels
-// could otherwise hold the CUs; every such wait is bounded anyway).
+// resident: they are chosen only when the launch gate (vp8g_device.h, GateScope) reports no other
+// launch of the library in flight, and every later launch on another stream is ordered after them.
 int run_locked(DevState& g_dev, const std::vector<Vp8gFrameDesc>& descs, const Vp8gBatchArrays& arr, uint8_t* d_out, hipStream_t s,
                uint32_t waves_hint, uint8_t* d_descs, bool may_split) {
 	uint32_t max_cols = 0, max_rows = 0;
@@ -238,65 +339,75 @@ int run_locked(DevState& g_dev, const std::vector<Vp8gFrameDesc>& descs, const V
 	const uint32_t n = (uint32_t)descs.size();
 	if (g_dev.pending) {  // the previous (asynchronous) launch on this context's buffers comes first
 		HIP_TRY(hipStreamWaitEvent(s, g_dev.done, 0), "hipStreamWaitEvent");
-		g_dev.pending = false;
 	}
 	if (!waves_hint) {
 		const char* e = getenv("VP8G_WAVES");  // override of the default waves per workgroup
 		if (e) waves_hint = (uint32_t)strtoul(e, nullptr, 10);
 	}
 	const uint32_t env = split_env();
-	const bool alone = g_pool.active.load() <= 1;  // (see above: cross-workgroup waits only when alone)
-	may_split = may_split && alone;
-	// small batches on the host APIs: 8-wave parts, up to kMaxSplit per frame (measured on one 4K
-	// frame: 8 waves x 8 parts 3.9 ms per call, 16 waves x 1..8 parts 8.1..4.7 ms)
+	// Buffers for every mode this call could pick, before the gate (growing may wait for this context's
+	// previous launch, or release idle contexts' buffers).
 	uint32_t nw = vp8g::pick_waves(waves_hint, max_rows, n);
-	if ((may_split || (env > 1 && alone)) && env != 1 && !waves_hint && vp8g::pick_split(env, n, 8, max_rows) > 1) nw = 8;
-	uint8_t* gctx = nullptr;
+	const bool try_split = (may_split || env > 1) && env != 1 && !waves_hint;
+	const uint32_t nw_split = try_split && vp8g::pick_split(env, n, 8, max_rows) > 1 ? 8u : nw;
 #ifdef VP8G_FORCE_GCTX  // diagnostic: per-column context in device memory for every frame
 	const bool big = true;
 #else
 	const bool big = vp8g::lds_bytes((int)nw, max_cols, false) > (size_t)vp8g::kMaxLds;
 #endif
+	const bool big_split = vp8g::lds_bytes((int)nw_split, max_cols, false) > (size_t)vp8g::kMaxLds;
+	uint8_t* gctx = nullptr;
 	if (big) {
 		const size_t need = descs.size() * (size_t)max_cols * vp8g::kCtxBytesPerCol;
-		HIP_TRY(grow(&g_dev.gctx, &g_dev.gctx_cap, need), "hipMalloc(ctx)");
+		HIP_TRY(grow(g_dev, &g_dev.gctx, &g_dev.gctx_cap, need), "hipMalloc(ctx)");
 		gctx = g_dev.gctx;
 	}
-	uint32_t k = 1;
-	if (!big && (may_split || (env > 1 && alone)) && env != 1) k = vp8g::pick_split(env, n, nw, max_rows);
-	uint8_t* mbox = nullptr;
-	uint32_t* gprog = nullptr;
+	const uint32_t k_want = !big_split && try_split ? vp8g::pick_split(env, n, nw_split, max_rows) : 1u;
+	if (k_want > 1) {
+		const size_t mb = (size_t)n * k_want * max_cols * vp8g::kCtxBytesPerCol, pb = (size_t)n * k_want * sizeof(uint32_t);
+		HIP_TRY(grow(g_dev, &g_dev.mbox, &g_dev.mbox_cap, mb + pb), "hipMalloc(mailbox)");
+	}
+	bool ordered = false;
+	const uint32_t wg = !big && !waves_hint ? vp8g::pick_chain(descs.data(), n, max_cols, &ordered) : 0u;
+	const bool split_want = wg && vp8g::pick_chain_split(n, max_cols, wg, ordered);
+	if (split_want) {
+		HIP_TRY(grow(g_dev, &g_dev.snap, &g_dev.snap_cap, (size_t)n * max_cols * vp8g::kCtxBytesPerCol), "hipMalloc(snapshots)");
+		const size_t old_cap = g_dev.sflags_cap;
+		HIP_TRY(grow(g_dev, &g_dev.sflags, &g_dev.sflags_cap, (size_t)n * sizeof(uint32_t)), "hipMalloc(flags)");
+		if (g_dev.sflags_cap != old_cap) g_dev.epoch = 0;  // (fresh flags: zeroed below)
+	}
+	g_dev.pending = false;
+
+	vp8g::GateScope gate(s);
+	HIP_TRY(gate.status(), "hipStreamWaitEvent(gate)");
+	const bool alone = gate.may_cross();
+	// small batches on the host APIs: 8-wave parts, up to kMaxSplit per frame (measured on one 4K
+	// frame: 8 waves x 8 parts 3.9 ms per call, 16 waves x 1..8 parts 8.1..4.7 ms)
+	const uint32_t k = alone && k_want > 1 ? k_want : 1u;
+	bool crossed = k > 1;
 	if (k > 1) {
 		const size_t mb = (size_t)n * k * max_cols * vp8g::kCtxBytesPerCol, pb = (size_t)n * k * sizeof(uint32_t);
-		HIP_TRY(grow(&g_dev.mbox, &g_dev.mbox_cap, mb + pb), "hipMalloc(mailbox)");
-		mbox = g_dev.mbox;
-		gprog = (uint32_t*)(g_dev.mbox + mb);
-		HIP_TRY(hipMemsetAsync(gprog, 0, pb, s), "memset(progress)");
-	}
-	if (!big && k == 1 && !waves_hint) {  // more frames than CUs: one 16-wave chain of frames per CU
-		bool ordered = false;
-		const uint32_t wg = vp8g::pick_chain(descs.data(), n, max_cols, &ordered);
-		if (wg) {
-			// mirror split (vp8g_kernels.hip, kSegTop): snapshot buffers and a fresh epoch for the flags
-			const bool split = alone && vp8g::pick_chain_split(n, max_cols, wg, ordered);
-			if (split) {
-				HIP_TRY(grow(&g_dev.snap, &g_dev.snap_cap, (size_t)n * max_cols * vp8g::kCtxBytesPerCol), "hipMalloc(snapshots)");
-				const size_t old_cap = g_dev.sflags_cap;
-				HIP_TRY(grow(&g_dev.sflags, &g_dev.sflags_cap, (size_t)n * sizeof(uint32_t)), "hipMalloc(flags)");
-				if (++g_dev.epoch == 0 || g_dev.sflags_cap != old_cap) {
-					if (g_dev.epoch == 0) g_dev.epoch = 1;
-					HIP_TRY(hipMemsetAsync(g_dev.sflags, 0, g_dev.sflags_cap, s), "memset(flags)");
-				}
-			}
-			HIP_TRY(vp8g::launch_chain((const Vp8gFrameDesc*)d_descs, n, arr, d_out, max_cols, s, wg, ordered, split, g_dev.snap,
-			                           (uint32_t*)g_dev.sflags, g_dev.epoch),
-			        "launch");
-			return 0;
+		HIP_TRY(hipMemsetAsync(g_dev.mbox + mb, 0, pb, s), "memset(progress)");
+		HIP_TRY(vp8g::launch_frames((const Vp8gFrameDesc*)d_descs, n, arr, d_out, max_cols, max_rows, nullptr, s, nw_split, k, g_dev.mbox,
+		                            (uint32_t*)(g_dev.mbox + mb), 0),
+		        "launch");
+	} else if (wg) {  // more frames than CUs: one 16-wave chain of frames per CU
+		// mirror split (vp8g_kernels.hip, kSegTop): snapshot flags of a fresh epoch
+		const bool split = alone && split_want;
+		if (split && (g_dev.epoch == 0 || ++g_dev.epoch == 0)) {  // (epoch 0 = the zeroed flags: never used)
+			g_dev.epoch = 1;
+			HIP_TRY(hipMemsetAsync(g_dev.sflags, 0, g_dev.sflags_cap, s), "memset(flags)");
 		}
+		crossed = split;
+		HIP_TRY(vp8g::launch_chain((const Vp8gFrameDesc*)d_descs, n, arr, d_out, max_cols, s, wg, ordered, split, g_dev.snap,
+		                           (uint32_t*)g_dev.sflags, g_dev.epoch),
+		        "launch");
+	} else {
+		const uint32_t ord = vp8g::pick_order(descs.data(), n, 1);  // cost-balanced placement (vp8g_device.h)
+		HIP_TRY(vp8g::launch_frames((const Vp8gFrameDesc*)d_descs, n, arr, d_out, max_cols, max_rows, gctx, s, nw, 1, nullptr, nullptr, ord),
+		        "launch");
 	}
-	const uint32_t ord = vp8g::pick_order(descs.data(), n, k);  // cost-balanced placement (vp8g_device.h)
-	HIP_TRY(vp8g::launch_frames((const Vp8gFrameDesc*)d_descs, n, arr, d_out, max_cols, max_rows, gctx, s, nw, k, mbox, gprog, ord),
-	        "launch");
+	HIP_TRY(gate.done(crossed), "hipEventRecord(gate)");
 	return 0;
 }
 
@@ -448,9 +559,9 @@ VP8G_API int vp8g_reconstruct_batch(const Vp8KeyFrameHeader* const* kfs, const V
 	} while (0)
 	TRY(dev_init(g_dev), "init");
 	const InLayout L = in_layout(mbs, 0);
-	TRY(grow(&g_dev.in, &g_dev.in_cap, L.total), "hipMalloc(in)");
-	TRY(grow(&g_dev.out, &g_dev.out_cap, outb ? outb : 256), "hipMalloc(out)");
-	TRY(grow(&g_dev.desc, &g_dev.desc_cap, n * sizeof(Vp8gFrameDesc)), "hipMalloc(desc)");
+	TRY(grow(g_dev, &g_dev.in, &g_dev.in_cap, L.total), "hipMalloc(in)");
+	TRY(grow(g_dev, &g_dev.out, &g_dev.out_cap, outb ? outb : 256), "hipMalloc(out)");
+	TRY(grow(g_dev, &g_dev.desc, &g_dev.desc_cap, n * sizeof(Vp8gFrameDesc)), "hipMalloc(desc)");
 	hipStream_t s = g_dev.stream;
 	uint8_t* in = g_dev.in;
 	for (uint32_t i = 0; i < n; i++) {
@@ -553,9 +664,9 @@ VP8G_API int vp8_loopfilter_apply_keyframe(Yuv420Image* img, const Vp8DecodedFra
 	DevState& g_dev = *lease.d;
 	HIP_TRY(dev_init(g_dev), "init");
 	const InLayout L = in_layout(k, frame_bytes);
-	HIP_TRY(grow(&g_dev.in, &g_dev.in_cap, L.total), "hipMalloc(in)");
-	HIP_TRY(grow(&g_dev.out, &g_dev.out_cap, frame_bytes), "hipMalloc(out)");
-	HIP_TRY(grow(&g_dev.desc, &g_dev.desc_cap, sizeof(Vp8gFrameDesc)), "hipMalloc(desc)");
+	HIP_TRY(grow(g_dev, &g_dev.in, &g_dev.in_cap, L.total), "hipMalloc(in)");
+	HIP_TRY(grow(g_dev, &g_dev.out, &g_dev.out_cap, frame_bytes), "hipMalloc(out)");
+	HIP_TRY(grow(g_dev, &g_dev.desc, &g_dev.desc_cap, sizeof(Vp8gFrameDesc)), "hipMalloc(desc)");
 	hipStream_t s = g_dev.stream;
 	uint8_t* in = g_dev.in;
 	const uint32_t cw = img->width / 2, ch = img->height / 2;
