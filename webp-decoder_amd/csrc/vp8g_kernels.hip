@@ -65,6 +65,9 @@ constexpr int kPrioTab[11] = {VP8G_PRIO_TABLE, VP8G_PRIO_LF, VP8G_PRIO_WHT};
 #ifndef VP8G_COMPACT  // iDCT: blocks with AC compacted two lanes per block when at most 32 in the wave
 #define VP8G_COMPACT 0
 #endif
+#ifndef VP8G_IDCT_C01  // iDCT: a cheaper transform when columns 2 and 3 of every block of the wave are zero
+#define VP8G_IDCT_C01 0
+#endif
 #ifndef VP8G_KATTR  // (experiments: e.g. __attribute__((amdgpu_num_vgpr(112))) to probe the register budget)
 #define VP8G_KATTR
 #endif
@@ -619,8 +622,13 @@ struct Pref {
 #ifndef VP8G_WPS8  // (experiments: waves per SIMD the 8-wave kernel is compiled for -- 6 = 80 VGPRs, three frames per CU)
 #define VP8G_WPS8 4
 #endif
+#ifndef VP8G_WPS12  // (experiments: the 12-wave kernel at 6 waves per SIMD = 80 VGPRs, two frames per CU)
+#define VP8G_WPS12 4
+#endif
 template <int NW>
-constexpr int min_waves_per_simd() { return NW == 10 ? 5 : (NW == 8 ? VP8G_WPS8 : (NW >= 6 ? 4 : (NW >= 2 ? (2 * NW) / 4 : 1))); }
+constexpr int min_waves_per_simd() {
+	return NW == 10 ? 5 : (NW == 8 ? VP8G_WPS8 : (NW == 12 ? VP8G_WPS12 : (NW >= 6 ? 4 : (NW >= 2 ? (2 * NW) / 4 : 1))));
+}
 
 // Split mode (kS, small batches): a frame's MB row pairs are dealt over `nsplit` workgroups
 // ("parts") of NW waves each -- global wave g = part * NW + wave owns pairs g, g + nsplit*NW, ...
@@ -1223,6 +1231,21 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 				};
 				if (mac == 0ull) {
 					dc_fill();
+#if VP8G_IDCT_C01
+				} else if (__ballot(act && ln < 24 && (w[1] | w[3] | w[5] | w[7]) != 0u) == 0ull) {
+					// Columns 2 and 3 of every block of the wave are zero (the vertical pass leaves them
+					// zero): the vertical pass of column pair 0 only, and the horizontal pass with
+					// x2 = x3 = 0 -- a1 = b1 = x0 + 4, c1 = mul_s(x1), d1 = mul_c(x1)
+					uint32_t oh[4];
+					vpass(w[0], w[2], w[4], w[6], oh);
+#pragma unroll
+					for (int r = 0; r < 4; r++) {
+						const int x0 = lo_s16(oh[r]) + 4, x1 = hi_s16(oh[r]);
+						const int c1 = mul_s(x1), d1 = mul_c(x1);
+						rs[2 * r] = pack2((x0 + d1) >> 3, (x0 + c1) >> 3);
+						rs[2 * r + 1] = pack2((x0 - c1) >> 3, (x0 - d1) >> 3);
+					}
+#endif
 				} else if (VP8G_COMPACT && __popcll(mac) <= 32) {
 					uint8_t* const wvb = smem + kHdrBytes + wave * kWaveBytes;
 					auto slot = [&](uint32_t q) { return wvb + (q >> 4) * (uint32_t)kHalfBytes + kResid + (q & 15u) * 32u; };
