@@ -32,6 +32,7 @@ sec = "pre"
 counts = collections.OrderedDict()
 def cls(op):
     if op.startswith("v_readlane") or op.startswith("v_writelane"): return "spill"
+    if op.startswith("scratch_"): return "scratch"
     if op.startswith("v_") : return "valu"
     if op.startswith("s_cbranch") or op.startswith("s_branch"): return "branch"
     if op.startswith("s_waitcnt") or op.startswith("s_sleep") or op.startswith("s_nop"): return "wait"
@@ -51,6 +52,7 @@ for l in body:
     counts.setdefault(sec, collections.Counter())[cls(op)] += 1
 names = {"pre": "prologue/pair setup", "after_30": "side info+residual+prefetch", "after_0": "wait", "after_1": "borders", "after_2": "predict+bpred",
          "after_3": "save ctx", "after_4": "loop filter", "after_5": "flush", "after_6": "publish/loop"}
-print("%-26s %6s %6s %6s %6s %6s %6s %6s" % ("section", "valu", "salu", "branch", "lds", "vmem", "wait", "lanes"))
+print("%-26s %6s %6s %6s %6s %6s %6s %6s %7s" % ("section", "valu", "salu", "branch", "lds", "vmem", "wait", "lanes", "scratch"))
 for k, c in counts.items():
-    print("%-26s %6d %6d %6d %6d %6d %6d %6d" % (names.get(k, k), c["valu"], c["salu"], c["branch"], c["lds"], c["vmem"], c["wait"], c["spill"]))
+    print("%-26s %6d %6d %6d %6d %6d %6d %6d %7d" % (names.get(k, k), c["valu"], c["salu"], c["branch"], c["lds"], c["vmem"], c["wait"], c["spill"],
+                                                  c["scratch"]))

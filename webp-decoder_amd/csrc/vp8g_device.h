@@ -100,9 +100,28 @@ inline size_t lds_bytes(int waves, uint32_t ctx_cols, bool global_ctx) {
 }
 // Chain mode (one 16-wave workgroup per CU decoding a list of frames, vp8g_kernels.hip): two
 // context slots and the list (at most list_max frames).
-constexpr int kChainWaves = 16;
-inline size_t chain_lds_bytes(uint32_t ctx_cols, uint32_t list_max) {
-	return (size_t)kHdrBytes + (size_t)kChainWaves * kWaveBytes + 2 * (size_t)ctx_cols * kCtxBytesPerCol + 4 * (size_t)list_max;
+// Experiment builds: VP8G_CHAIN_G = 1 keeps the chain's per-column context in device memory (one
+// region per frame; the LDS then holds only the cost sort's scratch), which lets VP8G_CHAIN_WPC
+// workgroups of VP8G_CHAIN_NW waves share a CU (e.g. 2 x 12 waves at 6 waves per SIMD).
+#ifndef VP8G_CHAIN_NW
+#define VP8G_CHAIN_NW 16
+#endif
+#ifndef VP8G_CHAIN_G
+#define VP8G_CHAIN_G 0
+#endif
+#ifndef VP8G_CHAIN_WPC
+#define VP8G_CHAIN_WPC 1
+#endif
+constexpr int kChainWaves = VP8G_CHAIN_NW;
+constexpr bool kChainG = VP8G_CHAIN_G != 0;
+constexpr int kChainWgPerCu = VP8G_CHAIN_WPC;
+// LDS context area of a chain workgroup: the two context slots, or (global context) the cost sort's
+// scratch of kCostClasses + n_frames words
+inline size_t chain_ctx_lds(uint32_t ctx_cols, uint32_t n_frames) {
+	return kChainG ? ((size_t)4 * (kCostClasses + n_frames) + 15) & ~(size_t)15 : 2 * (size_t)ctx_cols * kCtxBytesPerCol;
+}
+inline size_t chain_lds_bytes(uint32_t ctx_cols, uint32_t list_max, uint32_t n_frames) {
+	return (size_t)kHdrBytes + (size_t)kChainWaves * kWaveBytes + chain_ctx_lds(ctx_cols, n_frames) + 4 * (size_t)list_max;
 }
 
 // Process-wide launch gate (vp8g_shim.hip).  Launch modes whose workgroups wait on each other across

@@ -622,12 +622,15 @@ struct Pref {
 #ifndef VP8G_WPS8  // (experiments: waves per SIMD the 8-wave kernel is compiled for -- 6 = 80 VGPRs, three frames per CU)
 #define VP8G_WPS8 4
 #endif
+#ifndef VP8G_WPS16  // (experiments: the chain kernel's waves per SIMD; above 4 needs two workgroups per CU)
+#define VP8G_WPS16 4
+#endif
 #ifndef VP8G_WPS12  // (experiments: the 12-wave kernel at 6 waves per SIMD = 80 VGPRs, two frames per CU)
 #define VP8G_WPS12 4
 #endif
 template <int NW>
 constexpr int min_waves_per_simd() {
-	return NW == 10 ? 5 : (NW == 8 ? VP8G_WPS8 : (NW == 12 ? VP8G_WPS12 : (NW >= 6 ? 4 : (NW >= 2 ? (2 * NW) / 4 : 1))));
+	return NW == 10 ? 5 : (NW == 16 ? VP8G_WPS16 : NW == 8 ? VP8G_WPS8 : (NW == 12 ? VP8G_WPS12 : (NW >= 6 ? 4 : (NW >= 2 ? (2 * NW) / 4 : 1))));
 }
 
 // Split mode (kS, small batches): a frame's MB row pairs are dealt over `nsplit` workgroups
@@ -723,7 +726,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
                                                         uint8_t* __restrict__ gctx, uint32_t nsplit,
                                                         uint8_t* __restrict__ mbox, uint32_t* __restrict__ gprog,
                                                         uint32_t ord_first, uint32_t n_chain) {
-	static_assert(!kC || (!kG && !kS), "chain mode keeps the context in LDS and never splits");
+	static_assert(!kC || !kS, "chain mode never splits frames into parts");
 	extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 	const int lane0 = (int)(threadIdx.x & 63);
 	const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -731,7 +734,8 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 	const uint32_t nfr = kS ? gridDim.x / K : gridDim.x;
 	const uint32_t slot_bytes = ctx_cols * (uint32_t)kCtxBytesPerCol;
 	uint8_t* const ctx_base = smem + kHdrBytes + NW * kWaveBytes;
-	uint32_t* const chain_list = (uint32_t*)(ctx_base + 2 * slot_bytes);  // (kC) after the two context slots
+	// (kC) after the two context slots (global context: after the cost sort's scratch)
+	uint32_t* const chain_list = (uint32_t*)(ctx_base + (kG ? ((4u * (kCostClasses + n_chain) + 15u) & ~15u) : 2u * slot_bytes));
 	uint32_t m_chain = 1;  // (kC) frames in this workgroup's list
 	uint32_t f;
 	if constexpr (kC) {
@@ -966,11 +970,12 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 					wait_prog(last2 % NW, (last2 << kProgShift) + T2, false);
 				}
 				if (tag == kSegBottom) {
-					// the rows above come from the top segment's snapshot (another workgroup)
+					// the rows above come from the top segment's snapshot (another workgroup); with the
+					// context in device memory the snapshot is the frame's context itself
 					uint32_t* const flag = gprog + fcur;
 					if (!dead) wait_flag(flag, nsplit);
 					const uint8_t* const src = gctx + (size_t)fcur * slot_bytes;
-					for (uint32_t o = (uint32_t)lane0 * 16u; o < C * (uint32_t)kCtxBytesPerCol; o += 1024u) {
+					for (uint32_t o = (uint32_t)lane0 * 16u; !kG && o < C * (uint32_t)kCtxBytesPerCol; o += 1024u) {
 						const uint32_t* q = (const uint32_t*)(src + o);
 						st128(ctx.lds + o, u32x4{__hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
 						                         __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
@@ -1762,7 +1767,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 				// is final -> snapshot (write-through stores, drained) -> flag = this launch's epoch
 				asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 				uint8_t* const dst = gctx + (size_t)fcur * slot_bytes;
-				for (uint32_t o = (uint32_t)lane0 * 16u; o < C * (uint32_t)kCtxBytesPerCol; o += 1024u) {
+				for (uint32_t o = (uint32_t)lane0 * 16u; !kG && o < C * (uint32_t)kCtxBytesPerCol; o += 1024u) {
 					const u32x4 v = ld128(ctx.lds + o);
 					uint32_t* q = (uint32_t*)(dst + o);
 					__hip_atomic_store(q, v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1929,14 +1934,15 @@ uint32_t pick_chain(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint32_t ct
 	*ordered = false;
 	const int n_cus = device_cus();
 	if (mode == 0 || n_cus <= 0 || n_frames == 0 || (mode < 0 && n_frames <= (uint32_t)n_cus)) return 0;
-	const uint32_t wg = n_frames < (uint32_t)n_cus ? n_frames : (uint32_t)n_cus;
+	const uint32_t slots = (uint32_t)n_cus * (uint32_t)kChainWgPerCu;
+	const uint32_t wg = n_frames < slots ? n_frames : slots;
 	const uint32_t list_max = (n_frames + wg - 1) / wg;
-	if (ctx_cols > 1024 || chain_lds_bytes(ctx_cols, list_max) > (size_t)kMaxLds) return 0;
+	if (ctx_cols > 1024 || (size_t)kChainWgPerCu * chain_lds_bytes(ctx_cols, list_max, n_frames) > (size_t)kMaxLds) return 0;
 	// cost-class placement when the classes differ and the sort scratch fits the context slots
 	const uint32_t c0 = cost_class(h_descs[0]);
 	bool differ = false;
 	for (uint32_t i = 1; i < n_frames && !differ; i++) differ = cost_class(h_descs[i]) != c0;
-	*ordered = differ && (size_t)4 * (kCostClasses + n_frames) <= 2 * (size_t)ctx_cols * kCtxBytesPerCol && pick_order(h_descs, n_frames, 1) != 0;
+	*ordered = differ && (size_t)4 * (kCostClasses + n_frames) <= chain_ctx_lds(ctx_cols, n_frames) && pick_order(h_descs, n_frames, 1) != 0;
 	return wg;
 }
 
@@ -1950,7 +1956,7 @@ bool pick_chain_split(uint32_t n_frames, uint32_t ctx_cols, uint32_t workgroups,
 	}();
 	if (mode == 0 || workgroups == 0) return false;
 	const uint32_t list_max = (n_frames + workgroups - 1) / workgroups;
-	if (chain_lds_bytes(ctx_cols, 2 * list_max) > (size_t)kMaxLds) return false;
+	if ((size_t)kChainWgPerCu * chain_lds_bytes(ctx_cols, 2 * list_max, n_frames) > (size_t)kMaxLds) return false;
 	return mode > 0 || (ordered && list_max <= 2);
 }
 
@@ -1958,15 +1964,17 @@ hipError_t launch_chain(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const V
                         uint32_t ctx_cols, hipStream_t stream, uint32_t workgroups, bool ordered, bool split, uint8_t* snap,
                         uint32_t* flags, uint32_t epoch) {
 	if (n_frames == 0) return hipSuccess;
-	if (split && (!snap || !flags)) return hipErrorInvalidValue;
+	if ((split && (!snap || !flags)) || (kChainG && !snap)) return hipErrorInvalidValue;
 	const uint32_t list_max = (n_frames + workgroups - 1) / workgroups;
-	const size_t lds = chain_lds_bytes(ctx_cols, split ? 2 * list_max : list_max);
-	auto fn = frame_kernel<kChainWaves, false, false, true>;
-	hipError_t e = lds_attr<kChainWaves, false, false, true>();
+	const size_t lds = chain_lds_bytes(ctx_cols, split ? 2 * list_max : list_max, n_frames);
+	auto fn = frame_kernel<kChainWaves, kChainG, false, true>;
+	hipError_t e = lds_attr<kChainWaves, kChainG, false, true>();
 	if (e != hipSuccess) return e;
-	// (chain kernel arguments: gctx = snapshots, gprog = flags, nsplit = epoch, ord_first = ordered | split << 1)
+	// (chain kernel arguments: gctx = snapshots -- with the context in device memory, the frames'
+	// contexts, n_frames x ctx_cols x kCtxBytesPerCol --, gprog = flags, nsplit = epoch,
+	// ord_first = ordered | split << 1)
 	hipLaunchKernelGGL(fn, dim3(workgroups), dim3(kChainWaves * 64), lds, stream, d_descs, arrays, d_out, ctx_cols,
-	                   split ? snap : nullptr, split ? epoch : 1u, nullptr, split ? flags : nullptr,
+	                   split || kChainG ? snap : nullptr, split ? epoch : 1u, nullptr, split ? flags : nullptr,
 	                   (ordered ? 1u : 0u) | (split ? 2u : 0u), n_frames);
 	return hipGetLastError();
 }

@@ -370,6 +370,8 @@ int run_locked(DevState& g_dev, const std::vector<Vp8gFrameDesc>& descs, const V
 	bool ordered = false;
 	const uint32_t wg = !big && !waves_hint ? vp8g::pick_chain(descs.data(), n, max_cols, &ordered) : 0u;
 	const bool split_want = wg && vp8g::pick_chain_split(n, max_cols, wg, ordered);
+	if (wg && vp8g::kChainG)  // (experiment builds: the chain's context in device memory, in the snapshot buffer)
+		HIP_TRY(grow(g_dev, &g_dev.snap, &g_dev.snap_cap, (size_t)n * max_cols * vp8g::kCtxBytesPerCol), "hipMalloc(context)");
 	if (split_want) {
 		HIP_TRY(grow(g_dev, &g_dev.snap, &g_dev.snap_cap, (size_t)n * max_cols * vp8g::kCtxBytesPerCol), "hipMalloc(snapshots)");
 		const size_t old_cap = g_dev.sflags_cap;
