@@ -1684,6 +1684,16 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 				cl0 = ldc64(srcC);
 				if (okcc && (int)lcx > 0x3FFFFFFF) ctx.wr64(lcx + (t160 - 0x40000000u), cl0);
 				offC = okcc ? fl_offC + t * 8u : kNoStore;
+#if VP8G_ABLATE & 16
+				// diagnostic (output wrong): the same stores of the same lanes, linearised per wave half, so
+				// each step's pieces fill whole consecutive lines -- the traffic and time without partial lines
+				{
+					const uint32_t linR = ((H * sy) / (2 * NW)) & ~1023u, linRc = ((vofs + suv * CH) / (2 * NW)) & ~1023u;
+					const uint32_t reg = (uint32_t)(wave * 2 + hh), st = k * T + t;
+					offY = offY == kNoStore ? kNoStore : reg * linR + (st * 512u + (uint32_t)ln * 16u) % linR;
+					offC = offC == kNoStore ? kNoStore : reg * linRc + (st * 256u + (uint32_t)ln * 8u) % linRc;
+				}
+#endif
 			}
 #endif
 			else {
