@@ -60,6 +60,9 @@ WORKLOADS = {
     "uhd4": {"kind": "fixtures", "fixtures": UHD, "width": 3840, "height": 2160, "frames": 512},
     "fhd4": {"kind": "fixtures", "fixtures": FHD, "width": 1920, "height": 1080, "frames": 2048},
     "synth": {"kind": "synth", "width": 3840, "height": 2160, "frames": 512, "seed": 0x5EED, "profile": 0},
+    # (diagnostics, not reported: synthetic 1280x720 frames, small enough for two chain workgroups per CU
+    # with LDS context -- the occupancy experiment of DESIGN.md §5; outputs compared across builds)
+    "synth720": {"kind": "synth", "width": 1280, "height": 720, "frames": 2048, "seed": 0x5EED, "profile": 0},
     # BASELINE configs[1] semantics (-yuv, m06 only: no loop filter) on the uhd4 batch
     "uhd4_yuv": {"kind": "fixtures", "fixtures": UHD, "width": 3840, "height": 2160, "frames": 512, "unfiltered": True},
 }

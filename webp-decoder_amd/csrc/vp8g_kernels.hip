@@ -66,7 +66,7 @@ constexpr int kPrioTab[11] = {VP8G_PRIO_TABLE, VP8G_PRIO_LF, VP8G_PRIO_WHT};
 #define VP8G_COMPACT 0
 #endif
 #ifndef VP8G_IDCT_C01  // iDCT: a cheaper transform when columns 2 and 3 of every block of the wave are zero
-#define VP8G_IDCT_C01 0
+#define VP8G_IDCT_C01 1
 #endif
 #ifndef VP8G_KATTR  // (experiments: e.g. __attribute__((amdgpu_num_vgpr(112))) to probe the register budget)
 #define VP8G_KATTR
@@ -82,6 +82,9 @@ constexpr int kPrioTab[11] = {VP8G_PRIO_TABLE, VP8G_PRIO_LF, VP8G_PRIO_WHT};
 // ends the launch promptly with VP8G_ERR_TIMEOUT (tests/test_gpu_batch.py).
 #ifndef VP8G_WAIT_TICKS
 #define VP8G_WAIT_TICKS 200000000ull
+#endif
+#ifndef VP8G_WAIT_SLEEP  // s_sleep units (64 clocks each) between polls of a dependency wait
+#define VP8G_WAIT_SLEEP 1
 #endif
 #ifndef VP8G_TEST_STALL_WAVE
 #define VP8G_TEST_STALL_WAVE (-1)
@@ -894,7 +897,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 		uint64_t t0 = 0;
 		while (((kS && xin_) ? __hip_atomic_load(gp_in, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
 		             : __hip_atomic_load(prog + pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < need) {
-			__builtin_amdgcn_s_sleep(1);
+			__builtin_amdgcn_s_sleep(VP8G_WAIT_SLEEP);
 			if ((++spins & 1023u) == 0) {
 				const uint64_t now = __builtin_amdgcn_s_memrealtime();
 				if (t0 == 0) t0 = now;
