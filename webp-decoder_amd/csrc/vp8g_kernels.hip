@@ -368,6 +368,8 @@ DEV Rsrc plane_rsrc(uint8_t* base, uint32_t bytes) {
 #ifndef VP8G_STORE_AUX  // cache-policy bits of the output pixel stores (A/B experiments)
 #define VP8G_STORE_AUX 0
 #endif
+constexpr int kCpolSc1 = 16;   // cache-policy bits of a buffer access: sc1 (device-coherent, bypasses the CU's L1)
+constexpr int kSnapBatch = 8;  // mirror split: 16-B snapshot loads per lane in flight
 DEV void bst128(Rsrc r, uint32_t off, u32x4 v) { __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, VP8G_STORE_AUX); }
 DEV void bst64(Rsrc r, uint32_t off, u32x2 v) { __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)off, 0, VP8G_STORE_AUX); }
 
@@ -977,13 +979,17 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 					// context in device memory the snapshot is the frame's context itself
 					uint32_t* const flag = gprog + fcur;
 					if (!dead) wait_flag(flag, nsplit);
-					const uint8_t* const src = gctx + (size_t)fcur * slot_bytes;
-					for (uint32_t o = (uint32_t)lane0 * 16u; !kG && o < C * (uint32_t)kCtxBytesPerCol; o += 1024u) {
-						const uint32_t* q = (const uint32_t*)(src + o);
-						st128(ctx.lds + o, u32x4{__hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-						                         __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-						                         __hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-						                         __hip_atomic_load(q + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)});
+					// (16-B agent-coherent loads, kSnapBatch per lane in flight: one round trip per batch instead
+					// of one per 1 KB -- the chain's next pairs wait for this copy)
+					const uint32_t nb = C * (uint32_t)kCtxBytesPerCol;
+					const Rsrc rsn = plane_rsrc(gctx + (size_t)fcur * slot_bytes, nb);
+					for (uint32_t o0 = (uint32_t)lane0 * 16u; !kG && o0 < nb; o0 += 1024u * kSnapBatch) {
+						u32x4 v[kSnapBatch];
+#pragma unroll
+						for (int i = 0; i < kSnapBatch; i++) v[i] = __builtin_amdgcn_raw_buffer_load_b128(rsn, (int)(o0 + 1024u * i), 0, kCpolSc1);
+#pragma unroll
+						for (int i = 0; i < kSnapBatch; i++)
+							if (o0 + 1024u * i < nb) st128(ctx.lds + o0 + 1024u * i, v[i]);
 					}
 				}
 				put_tables(*Dp, tabo, lane0);
@@ -1779,14 +1785,15 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 				// top segment of a mirror-split frame, last step of its last pair: every column's context
 				// is final -> snapshot (write-through stores, drained) -> flag = this launch's epoch
 				asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-				uint8_t* const dst = gctx + (size_t)fcur * slot_bytes;
-				for (uint32_t o = (uint32_t)lane0 * 16u; !kG && o < C * (uint32_t)kCtxBytesPerCol; o += 1024u) {
-					const u32x4 v = ld128(ctx.lds + o);
-					uint32_t* q = (uint32_t*)(dst + o);
-					__hip_atomic_store(q, v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-					__hip_atomic_store(q + 1, v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-					__hip_atomic_store(q + 2, v.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-					__hip_atomic_store(q + 3, v.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+				const uint32_t nb = C * (uint32_t)kCtxBytesPerCol;
+				const Rsrc rsn = plane_rsrc(gctx + (size_t)fcur * slot_bytes, nb);
+				for (uint32_t o0 = (uint32_t)lane0 * 16u; !kG && o0 < nb; o0 += 1024u * kSnapBatch) {
+					u32x4 v[kSnapBatch];
+#pragma unroll
+					for (int i = 0; i < kSnapBatch; i++) v[i] = ld128(ctx.lds + min(o0 + 1024u * i, nb - 16u));
+#pragma unroll
+					for (int i = 0; i < kSnapBatch; i++)  // (sc1: write-through to the device-coherent level; lanes past the end dropped)
+						__builtin_amdgcn_raw_buffer_store_b128(v[i], rsn, (int)(o0 + 1024u * i), 0, kCpolSc1);
 				}
 				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 				if (lane0 == 0) __hip_atomic_store(gprog + fcur, nsplit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
