@@ -62,7 +62,7 @@ WORKLOADS = {
     "synth": {"kind": "synth", "width": 3840, "height": 2160, "frames": 512, "seed": 0x5EED, "profile": 0},
     # (diagnostics, not reported: synthetic 1280x720 frames, small enough for two chain workgroups per CU
     # with LDS context -- the occupancy experiment of DESIGN.md §5; outputs compared across builds)
-    "synth720": {"kind": "synth", "width": 1280, "height": 720, "frames": 2048, "seed": 0x5EED, "profile": 0},
+    "synth720": {"kind": "synth", "width": 1280, "height": 720, "frames": 2048, "seed": 0x5EED, "profile": 0, "diagnostic": True},
     # BASELINE configs[1] semantics (-yuv, m06 only: no loop filter) on the uhd4 batch
     "uhd4_yuv": {"kind": "fixtures", "fixtures": UHD, "width": 3840, "height": 2160, "frames": 512, "unfiltered": True},
 }
@@ -581,7 +581,7 @@ def main(argv=None):
     torch.cuda.empty_cache()
     if world == 1 and args.extra == "auto":
         for name in WORKLOADS:
-            if name != args.workload:
+            if name != args.workload and not WORKLOADS[name].get("diagnostic"):
                 o = run_workload(name, args, rank, world, dist, dev, golden)
                 del o["_rank"]
                 torch.cuda.empty_cache()
