@@ -74,6 +74,13 @@ constexpr int kPrioTab[11] = {VP8G_PRIO_TABLE, VP8G_PRIO_LF, VP8G_PRIO_WHT};
 #ifndef VP8G_FAST_LF  // loop filter: line addresses from per-pair lane words (lf_vp / lf_hp)
 #define VP8G_FAST_LF 1
 #endif
+#ifndef VP8G_BP_REGION  // B_PRED: one exec region around the wavefront instead of one per step
+#define VP8G_BP_REGION 1
+#endif
+#ifndef VP8G_LF_REDIRECT  // loop filter: stores without exec regions (chroma lanes' extra bytes to scratch)
+#define VP8G_LF_REDIRECT 0
+#endif
+static_assert(!VP8G_LF_REDIRECT || VP8G_FAST_LF, "the store redirection's scratch bases come from the fast line addresses");
 #ifndef VP8G_LF_VPACK  // loop filter, vertical-edge pass: dword row gathers / scatters instead of byte accesses
 #define VP8G_LF_VPACK 0
 #endif
@@ -560,13 +567,16 @@ struct LfLine {
 	uint8_t* Lp;
 	uint8_t* Mp;
 	uint8_t* colp;
+	uint8_t* Mhi;    // (VP8G_LF_REDIRECT) base of a lane's row bytes 10..17: Mp, or scratch for chroma lanes
+	uint8_t* colhi;  // (VP8G_LF_REDIRECT) base of a lane's column bytes 10..17: colp, or scratch for chroma
 };
 DEV LfLine lf_lines(uint8_t* tY, uint8_t* tC, int ln, int slot) {
 	const bool isy = ln < 16;
 	const int cp = (ln >> 3) & 1;
 	uint8_t* const rowp = isy ? tY + (4 + ln) * kTP : tC + (4 + (ln & 7)) * kTP + cp * kCV;
 	const int off = isy ? slot * 16 : slot * 8, ring = isy ? 31 : 15;
-	return LfLine{rowp + ((off - 4) & ring), rowp + off, isy ? tY + slot * 16 + ln : tC + cp * kCV + slot * 8 + (ln & 7)};
+	uint8_t* const colp = isy ? tY + slot * 16 + ln : tC + cp * kCV + slot * 8 + (ln & 7);
+	return LfLine{rowp + ((off - 4) & ring), rowp + off, colp, rowp + off, colp};
 }
 template <bool kSimple>
 DEV void lf_mb(const LfLine& L, int ln, bool en, bool mb_v, bool mb_h, bool inner, int E, int I, int T) {
@@ -607,16 +617,23 @@ DEV void lf_mb(const LfLine& L, int ln, bool en, bool mb_v, bool mb_h, bool inne
 		gather20<1, 1>(Lp, Mp, px);
 		PRIO(9);
 		lf_line<kSimple>(px, en && mb_v, en && inner, isy, E, I, T);
-		if (wr) {
+		if (VP8G_LF_REDIRECT || wr) {
 #endif
 #pragma unroll
 			for (int i = 1; i < 4; i++) stb(Lp + i, px[i]);
 #pragma unroll
 			for (int i = 0; i < 6; i++) stb(Mp + i, px[4 + i]);
+#if VP8G_LF_REDIRECT
+			// (no exec regions: a lane that filters nothing writes its unchanged bytes back, and the
+			// chroma lanes' bytes past their 8-pixel row go to scratch)
+#pragma unroll
+			for (int i = 6; i < 14; i++) stb(L.Mhi + i, px[4 + i]);
+#else
 			if (isy) {
 #pragma unroll
 				for (int i = 6; i < 14; i++) stb(Mp + i, px[4 + i]);
 			}
+#endif
 		}
 	}
 	wave_lds_sync();
@@ -627,13 +644,18 @@ DEV void lf_mb(const LfLine& L, int ln, bool en, bool mb_v, bool mb_h, bool inne
 		gather20<kTP, kTP>(colp, colp + 4 * kTP, px);
 		PRIO(9);
 		lf_line<kSimple>(px, en && mb_h, en && inner, isy, E, I, T);
-		if (wr) {
+		if (VP8G_LF_REDIRECT || wr) {
 #pragma unroll
 			for (int i = 1; i < 10; i++) stb(colp + kTP * i, px[i]);
+#if VP8G_LF_REDIRECT
+#pragma unroll
+			for (int i = 10; i < 18; i++) stb(L.colhi + kTP * i, px[i]);
+#else
 			if (isy) {
 #pragma unroll
 				for (int i = 10; i < 18; i++) stb(colp + kTP * i, px[i]);
 			}
+#endif
 		}
 	}
 	wave_lds_sync();
@@ -1552,12 +1574,17 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 					const int16_t* const rsp = (const int16_t*)(hv + kResid) + p + 32 * g;    // + 16 b0
 					const u32x4* const tabp = (const u32x4*)(smem + kBpTable) + p * (kBpEntry / 16);  // + 16 mode entries
 					const bool col3 = cc == 3;
+#if VP8G_BP_REGION
+					// (one exec region for the whole wavefront: group 0 has a sub-block at every step and
+					// group 1 at steps 2..7, so only steps 0, 1, 8, 9 narrow the lanes again)
+					if (bp_lane) {
+#endif
 #pragma unroll
 					for (int s = 0; s < 10; s++) {
 						const int i0 = s <= 3 ? 0 : (s - 2) >> 1;
 						const int j0 = s - 2 * i0;  // g = 0: (i0, j0); g = 1: (i0 + 1, j0 - 2)
 						const bool v0 = j0 <= 3, v1 = i0 + 1 <= 3 && j0 >= 2;
-						const bool valid = bp_lane && (g ? v1 : v0);
+						const bool valid = (VP8G_BP_REGION || bp_lane) && (g ? v1 : v0);
 						if (valid) {
 							const int b0 = 4 * i0 + j0;
 							const int mb0 = v0 ? (int)((bmw[b0 >> 2] >> (8 * (b0 & 3))) & 0xFFu) : 0;
@@ -1600,6 +1627,9 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 						}
 						wave_lds_sync();
 					}
+#if VP8G_BP_REGION
+					}
+#endif
 				}
 			}
 			wave_lds_sync();
@@ -1626,6 +1656,11 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 						L.Mp = wv + __builtin_amdgcn_ubfe(lf_vp, sl16, 16u);
 						L.Lp = L.Mp + (slot ? -4 : (ln < 16 ? 28 : 12));
 						L.colp = wv + __builtin_amdgcn_ubfe(lf_hp, sl16, 16u);
+						// (VP8G_LF_REDIRECT) chroma lanes' bytes 10..17 land in the half's B_PRED residual area,
+						// free after B_PRED: 16 distinct dword-spaced bases per half
+						uint8_t* const scr = hv + kResid + 4 * (ln & 15);
+						L.Mhi = ln < 16 ? L.Mp : scr - 6;
+						L.colhi = ln < 16 ? L.colp : scr - 10 * kTP;
 					}
 #else
 					const LfLine L = lf_lines(tY, tC, ln, slot);
