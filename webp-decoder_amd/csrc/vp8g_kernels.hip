@@ -77,6 +77,9 @@ constexpr int kPrioTab[11] = {VP8G_PRIO_TABLE, VP8G_PRIO_LF, VP8G_PRIO_WHT};
 #ifndef VP8G_BP_REGION  // B_PRED: one exec region around the wavefront instead of one per step
 #define VP8G_BP_REGION 1
 #endif
+#ifndef VP8G_DQ_B128  // residual: the dequant factors of all four segments in one 16-B LDS read
+#define VP8G_DQ_B128 0
+#endif
 #ifndef VP8G_LF_REDIRECT  // loop filter: stores without exec regions (chroma lanes' extra bytes to scratch)
 #define VP8G_LF_REDIRECT 0
 #endif
@@ -869,7 +872,12 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 	uint32_t bt_l = kBorderTab.v[lane0 & 31];  // this lane's border-setup role (loop-invariant)
 	// dequant / loop-filter tables of a frame into its slot (chain mode: by the wave of the frame's pair 0)
 	auto put_tables = [&](const Vp8gFrameDesc& Df, uint32_t tabo, int l) {
-		if (l < 24) ((int16_t*)(smem + kDqTable + tabo))[l] = Df.dq[l / 6][l % 6];
+		// dequant factors as (dc, ac) int16 pairs, [class][segment] (VP8G_DQ_B128: one 16-B read per lane
+		// fetches a class's four segments before the segment is known) or [segment][class]
+		if (l < 24) {
+			const int sg = l / 6, k = l % 6, cl = k >> 1;
+			((int16_t*)(smem + kDqTable + tabo))[VP8G_DQ_B128 ? (cl * 4 + sg) * 2 + (k & 1) : l] = Df.dq[sg][k];
+		}
 		if (l < 32) smem[kLfTable + tabo + l] = Df.lf[l >> 3][(l >> 2) & 1][l & 3];
 	};
 	if constexpr (!kC) put_tables(descs[f], 0u, (int)threadIdx.x);
@@ -1198,6 +1206,10 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 			// per-half side info (lanes 26..29 / 58..61 hold it)
 			// per-half side info, held by lanes 26..29 / 58..61: fetched with ds_bpermute (LDS
 			// crossbar, no LDS memory) instead of readlane + per-half select
+#if VP8G_DQ_B128
+			// (the four segments' dequant factors of this lane's class, read before the side info is known)
+			const u32x4 dq4 = *(const u32x4*)(smem + kDqTable + tabo + 16 * (ln < 16 ? 0 : (ln < 24 ? 1 : 2)));
+#endif
 			const int sdl = (hh ? 58 : 26) * 4;
 			const int ymode = __builtin_amdgcn_ds_bpermute(sdl, (int)cur.side);
 			const int uvmode = __builtin_amdgcn_ds_bpermute(sdl + 4, (int)cur.side);
@@ -1227,8 +1239,19 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 				// vertical pass wrap mod 2^16 exactly like the reference's int16 stores; the
 				// horizontal pass (whose (x + 4) >> 3 needs the full-precision sum) runs in 32 bits.
 				const int cls = ln < 16 ? 0 : (ln < 24 ? 1 : 2);  // Y1, UV, Y2 factors
+#if VP8G_DQ_B128
+				uint32_t fdcac;  // (dc, ac) int16 pair: dq4[seg] by two v_cndmask levels
+				{
+					const uint64_t m1 = __builtin_amdgcn_ballot_w64((seg & 1) != 0), m2 = __builtin_amdgcn_ballot_w64((seg & 2) != 0);
+					uint32_t lo, hi;
+					asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(lo) : "v"(dq4.x), "v"(dq4.y), "s"(m1));
+					asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(hi) : "v"(dq4.z), "v"(dq4.w), "s"(m1));
+					asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(fdcac) : "v"(lo), "v"(hi), "s"(m2));
+				}
+#else
 				const uint32_t* dqt = (const uint32_t*)(smem + kDqTable + tabo) + seg * 3 + cls;
 				const uint32_t fdcac = *dqt;  // (dc, ac) int16 pair
+#endif
 				const uint32_t facac = __builtin_amdgcn_perm(fdcac, fdcac, 0x03020302u);
 				uint32_t w[8] = {pk_mul(cur.a.x, fdcac), pk_mul(cur.a.y, facac), pk_mul(cur.a.z, facac), pk_mul(cur.a.w, facac),
 				                 pk_mul(cur.b.x, facac), pk_mul(cur.b.y, facac), pk_mul(cur.b.z, facac), pk_mul(cur.b.w, facac)};
@@ -1445,8 +1468,10 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 					const bool ly = (bt >> 22) & 1u;
 					const uint32_t lo = rec_off(cu) + ((bt >> 12) & 0xFFu);
 					uint8_t* const td = hv + (bt & 0xFFFu) + (slot ? (ly ? 16u : 8u) : 0u);
-					if (ly) st64(td, ctx.rd64(lo)), st64(td + 8, ctx.rd64(lo + 8));
-					else stc64(td, ctx.rd64(lo));
+					// (both halves of a luma row loaded before either store: one LDS round trip, not two)
+					const u32x2 s0 = ctx.rd64(lo), s1 = ctx.rd64(lo + 8);
+					if (ly) st64(td, s0), st64(td + 8, s1);
+					else stc64(td, s0);
 #else
 					const bool ly = ln < 24;
 					const int p = (ln - 24) >> 2, tr = ly ? ln - 20 : (ln - 24) & 3;
