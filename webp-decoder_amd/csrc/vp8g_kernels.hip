@@ -62,9 +62,6 @@ constexpr int kPrioTab[11] = {VP8G_PRIO_TABLE, VP8G_PRIO_LF, VP8G_PRIO_WHT};
 #ifndef VP8G_FAST_STRIP  // borders: the filter-state copy of lanes 20..31 from kBorderTab roles
 #define VP8G_FAST_STRIP 1
 #endif
-#ifndef VP8G_COMPACT  // iDCT: blocks with AC compacted two lanes per block when at most 32 in the wave
-#define VP8G_COMPACT 0
-#endif
 #ifndef VP8G_IDCT_C01  // iDCT: a cheaper transform when columns 2 and 3 of every block of the wave are zero
 #define VP8G_IDCT_C01 1
 #endif
@@ -78,7 +75,7 @@ constexpr int kPrioTab[11] = {VP8G_PRIO_TABLE, VP8G_PRIO_LF, VP8G_PRIO_WHT};
 #define VP8G_BP_REGION 1
 #endif
 #ifndef VP8G_DQ_B128  // residual: the dequant factors of all four segments in one 16-B LDS read
-#define VP8G_DQ_B128 0
+#define VP8G_DQ_B128 1
 #endif
 #ifndef VP8G_LF_REDIRECT  // loop filter: stores without exec regions (chroma lanes' extra bytes to scratch)
 #define VP8G_LF_REDIRECT 0
@@ -1287,25 +1284,16 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 					if (ln < 16 && !bpred) w[0] = (w[0] & 0xFFFF0000u) | *(const uint16_t*)(hv + kWht + 2 * ln);
 					PRIO(0);
 				}
-				// inverse DCT (RFC 14.4).  DC-only shortcut when no lane of the wave has an AC coefficient
-				// ((dc+4)>>3 everywhere, exact).  With at most 32 blocks with AC in the wave (VP8G_COMPACT)
-				// the blocks are compacted, two lanes per block: the AC lanes stage their coefficients in
-				// the wave's kResid areas (slot q = rank among the AC lanes, 32 B: column halves 0 and
-				// 1), lane j transforms column half j & 1 of slot j >> 1 (vertical pass), swaps row halves
-				// with its partner lane (DPP), runs the horizontal pass on two rows and stores them back;
-				// the AC lanes read their rows.  Else the whole block per lane.
+				auto wht_dc = [&]() -> uint32_t { return 0u; };  // (round 4 measured adding the WHT's DC late, +0.5 %: DESIGN §6)
+				// inverse DCT (RFC 14.4), the whole block per lane.  DC-only shortcut when no lane of the wave
+				// has an AC coefficient ((dc+4)>>3 everywhere, exact); a column-pair-0 transform when no
+				// block of the wave has coefficients in columns 2-3.  (Round 3 compacted the AC blocks two
+				// lanes per block through LDS: +1.6 %, removed)
 				const uint64_t mac = __ballot(anyac && ln < 24 && act);
-				auto dc_fill = [&]() {
-					const int d = (lo_s16(w[0]) + 4) >> 3;
+				auto dc_fill = [&](uint32_t dcadd) {
+					const int d = (lo_s16(pk_add(w[0], dcadd)) + 4) >> 3;
 #pragma unroll
 					for (int i = 0; i < 8; i++) rs[i] = pack2(d, d);
-				};
-				auto hpass = [&](uint32_t lo, uint32_t hi, uint32_t& y0, uint32_t& y1) {  // one row
-					const int x0 = lo_s16(lo), x1 = hi_s16(lo), x2 = lo_s16(hi), x3 = hi_s16(hi);
-					const int a1 = x0 + x2 + 4, b1 = x0 - x2 + 4;
-					const int c1 = mul_s(x1) - mul_c(x3), d1 = mul_c(x1) + mul_s(x3);
-					y0 = pack2((a1 + d1) >> 3, (b1 + c1) >> 3);
-					y1 = pack2((b1 - c1) >> 3, (a1 - d1) >> 3);
 				};
 				auto vpass = [&](uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3, uint32_t* o) {  // two columns
 					const uint32_t a1 = pk_add(r0, r2), b1 = pk_sub(r0, r2);
@@ -1316,7 +1304,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 					o[2] = pk_sub(b1, c1);
 				};
 				if (mac == 0ull) {
-					dc_fill();
+					dc_fill(wht_dc());
 #if VP8G_IDCT_C01
 				} else if (__ballot(act && ln < 24 && (w[1] | w[3] | w[5] | w[7]) != 0u) == 0ull) {
 					// Columns 2 and 3 of every block of the wave are zero (the vertical pass leaves them
@@ -1324,47 +1312,20 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 					// x2 = x3 = 0 -- a1 = b1 = x0 + 4, c1 = mul_s(x1), d1 = mul_c(x1)
 					uint32_t oh[4];
 					vpass(w[0], w[2], w[4], w[6], oh);
+					int c1[4], d1[4];
 #pragma unroll
 					for (int r = 0; r < 4; r++) {
-						const int x0 = lo_s16(oh[r]) + 4, x1 = hi_s16(oh[r]);
-						const int c1 = mul_s(x1), d1 = mul_c(x1);
-						rs[2 * r] = pack2((x0 + d1) >> 3, (x0 + c1) >> 3);
-						rs[2 * r + 1] = pack2((x0 - c1) >> 3, (x0 - d1) >> 3);
+						const int x1 = hi_s16(oh[r]);
+						c1[r] = mul_s(x1), d1[r] = mul_c(x1);
+					}
+					const uint32_t dcadd = wht_dc();
+#pragma unroll
+					for (int r = 0; r < 4; r++) {
+						const int x0 = lo_s16(pk_add(oh[r], dcadd)) + 4;
+						rs[2 * r] = pack2((x0 + d1[r]) >> 3, (x0 + c1[r]) >> 3);
+						rs[2 * r + 1] = pack2((x0 - c1[r]) >> 3, (x0 - d1[r]) >> 3);
 					}
 #endif
-				} else if (VP8G_COMPACT && __popcll(mac) <= 32) {
-					uint8_t* const wvb = smem + kHdrBytes + wave * kWaveBytes;
-					auto slot = [&](uint32_t q) { return wvb + (q >> 4) * (uint32_t)kHalfBytes + kResid + (q & 15u) * 32u; };
-					const bool isac = (mac >> lane) & 1ull;
-					const uint32_t q = __builtin_amdgcn_mbcnt_hi((uint32_t)(mac >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mac, 0u));
-					if (isac) {
-						st128(slot(q), u32x4{w[0], w[2], w[4], w[6]});
-						st128(slot(q) + 16, u32x4{w[1], w[3], w[5], w[7]});
-					}
-					dc_fill();
-					wave_lds_sync();
-					{
-						const uint32_t jq = (uint32_t)lane >> 1;
-						const bool h = lane & 1;
-						uint8_t* const sp = slot(jq) + (h ? 16u : 0u);
-						const u32x4 in = ld128(sp);
-						uint32_t o[4];  // rows 0..3 of column half h
-						vpass(in.x, in.y, in.z, in.w, o);
-						// lane h = 0 keeps rows 0, 1 and takes columns 2, 3 of them from its partner; h = 1 rows 2, 3
-						const uint32_t rx = (uint32_t)__builtin_amdgcn_mov_dpp((int)(h ? o[0] : o[2]), 0xB1, 0xF, 0xF, false);
-						const uint32_t ry = (uint32_t)__builtin_amdgcn_mov_dpp((int)(h ? o[1] : o[3]), 0xB1, 0xF, 0xF, false);
-						uint32_t y0, y1, y2, y3;
-						hpass(h ? rx : o[0], h ? o[2] : rx, y0, y1);
-						hpass(h ? ry : o[1], h ? o[3] : ry, y2, y3);
-						st128(sp, u32x4{y0, y1, y2, y3});
-					}
-					wave_lds_sync();
-					if (isac) {
-						const u32x4 lo = ld128(slot(q)), hi = ld128(slot(q) + 16);
-						rs[0] = lo.x, rs[1] = lo.y, rs[2] = lo.z, rs[3] = lo.w;
-						rs[4] = hi.x, rs[5] = hi.y, rs[6] = hi.z, rs[7] = hi.w;
-					}
-					wave_lds_sync();
 				} else {
 					uint32_t o[8];
 #pragma unroll
@@ -1374,8 +1335,22 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 #pragma unroll
 						for (int r = 0; r < 4; r++) o[2 * r + h] = oh[r];
 					}
+					// horizontal pass: the multiplications first (columns 1, 3), then the sums with column 0
+					// (which carries the late DC) and column 2
+					int c1[4], d1[4];
 #pragma unroll
-					for (int r = 0; r < 4; r++) hpass(o[2 * r], o[2 * r + 1], rs[2 * r], rs[2 * r + 1]);  // horizontal pass
+					for (int r = 0; r < 4; r++) {
+						const int x1 = hi_s16(o[2 * r]), x3 = hi_s16(o[2 * r + 1]);
+						c1[r] = mul_s(x1) - mul_c(x3), d1[r] = mul_c(x1) + mul_s(x3);
+					}
+					const uint32_t dcadd = wht_dc();
+#pragma unroll
+					for (int r = 0; r < 4; r++) {
+						const int x0 = lo_s16(pk_add(o[2 * r], dcadd)), x2 = lo_s16(o[2 * r + 1]);
+						const int a1 = x0 + x2 + 4, b1 = x0 - x2 + 4;
+						rs[2 * r] = pack2((a1 + d1[r]) >> 3, (b1 + c1[r]) >> 3);
+						rs[2 * r + 1] = pack2((b1 - c1[r]) >> 3, (a1 - d1[r]) >> 3);
+					}
 				}
 				if (ln < 16) {
 					uint8_t* rp = hv + kResid + ln * 32;
