@@ -1235,7 +1235,6 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 				// Packed int16 pairs: w[2r + h] = row r, columns 2h, 2h+1.  Dequantisation and the
 				// vertical pass wrap mod 2^16 exactly like the reference's int16 stores; the
 				// horizontal pass (whose (x + 4) >> 3 needs the full-precision sum) runs in 32 bits.
-				const int cls = ln < 16 ? 0 : (ln < 24 ? 1 : 2);  // Y1, UV, Y2 factors
 #if VP8G_DQ_B128
 				uint32_t fdcac;  // (dc, ac) int16 pair: dq4[seg] by two v_cndmask levels
 				{
@@ -1246,6 +1245,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 					asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(fdcac) : "v"(lo), "v"(hi), "s"(m2));
 				}
 #else
+				const int cls = ln < 16 ? 0 : (ln < 24 ? 1 : 2);  // Y1, UV, Y2 factors
 				const uint32_t* dqt = (const uint32_t*)(smem + kDqTable + tabo) + seg * 3 + cls;
 				const uint32_t fdcac = *dqt;  // (dc, ac) int16 pair
 #endif
