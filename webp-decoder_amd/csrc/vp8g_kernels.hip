@@ -74,6 +74,9 @@ constexpr int kPrioTab[11] = {VP8G_PRIO_TABLE, VP8G_PRIO_LF, VP8G_PRIO_WHT};
 #ifndef VP8G_BP_REGION  // B_PRED: one exec region around the wavefront instead of one per step
 #define VP8G_BP_REGION 1
 #endif
+#ifndef VP8G_PRED_FLAT  // whole-block predictor: DC sums without a branch, all loads in one round trip
+#define VP8G_PRED_FLAT 0
+#endif
 #ifndef VP8G_DQ_B128  // residual: the dequant factors of all four segments in one 16-B LDS read
 #define VP8G_DQ_B128 1
 #endif
@@ -1481,14 +1484,6 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 #endif
 					const int mode = yl ? (ymode > 4 ? 0 : ymode) : (uvmode > 3 ? 0 : uvmode);
 					const u32x2 a01 = ld64(ab), a23 = ld64(ab + 8), l01 = ld64(lc), l23 = ld64(lc + 8);
-					const uint32_t sa2 = __builtin_amdgcn_sad_u8(a01.y, 0u, __builtin_amdgcn_sad_u8(a01.x, 0u, 0u));
-					const uint32_t sl2 = __builtin_amdgcn_sad_u8(l01.y, 0u, __builtin_amdgcn_sad_u8(l01.x, 0u, 0u));
-					const uint32_t sa4 = __builtin_amdgcn_sad_u8(a23.y, 0u, __builtin_amdgcn_sad_u8(a23.x, 0u, sa2));
-					const uint32_t sl4 = __builtin_amdgcn_sad_u8(l23.y, 0u, __builtin_amdgcn_sad_u8(l23.x, 0u, sl2));
-					const bool ha = r > 0, hl = c > 0;
-					const uint32_t sum = (ha ? (yl ? sa4 : sa2) : 0u) + (hl ? (yl ? sl4 : sl2) : 0u);
-					const int shift = (yl ? 3 : 2) + (ha ? 1 : 0) + (hl ? 1 : 0);  // 16 or 8 samples per edge
-					const int dcv = (ha || hl) ? (int)((sum + (1u << (shift - 1))) >> shift) : 128;
 #if VP8G_PRED_ROLE
 					const uint32_t aw = ld32(hv + __builtin_amdgcn_ubfe(prole.x, 11u, 11u));
 					const uint32_t lw = ld32(lc + 4u * __builtin_amdgcn_ubfe(prole.y, 22u, 2u));
@@ -1497,6 +1492,21 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 					const uint32_t lw = ld32(lc + 4 * by);
 #endif
 					const int P = (int)ab[-1];
+					const uint32_t sa2 = __builtin_amdgcn_sad_u8(a01.y, 0u, __builtin_amdgcn_sad_u8(a01.x, 0u, 0u));
+					const uint32_t sl2 = __builtin_amdgcn_sad_u8(l01.y, 0u, __builtin_amdgcn_sad_u8(l01.x, 0u, 0u));
+					const uint32_t sa4 = __builtin_amdgcn_sad_u8(a23.y, 0u, __builtin_amdgcn_sad_u8(a23.x, 0u, sa2));
+					const uint32_t sl4 = __builtin_amdgcn_sad_u8(l23.y, 0u, __builtin_amdgcn_sad_u8(l23.x, 0u, sl2));
+					const bool ha = r > 0, hl = c > 0;
+					const uint32_t sum = (ha ? (yl ? sa4 : sa2) : 0u) + (hl ? (yl ? sl4 : sl2) : 0u);
+					const int shift = (yl ? 3 : 2) + (ha ? 1 : 0) + (hl ? 1 : 0);  // 16 or 8 samples per edge
+#if VP8G_PRED_FLAT
+					// (no branch around the sums: every load of the predictor issued in one LDS round trip)
+					int dcv;
+					asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(dcv) : "v"(128), "v"((int)((sum + (1u << (shift - 1))) >> shift)),
+					    "s"(__builtin_amdgcn_ballot_w64(ha || hl)));
+#else
+					const int dcv = (ha || hl) ? (int)((sum + (1u << (shift - 1))) >> shift) : 128;
+#endif
 					// two pixels per op as int16 pairs (|residual| < 2^14, so nothing wraps)
 					const uint32_t mA = (mode == 1 || mode == 3) ? 0x00FF00FFu : 0u;
 					const uint32_t mL = (mode == 2 || mode == 3) ? 0x00FF00FFu : 0u;
