@@ -317,3 +317,28 @@ def test_device_batches_two_streams_and_dropin_concurrently(vp8g, digests):
         f.free()
     del batches
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("w,h", [(160, 96), (176, 80)])
+def test_chain_two_frame_interleave(vp8g, w, h):
+    """Two-frame interleave of the chain (vp8g_kernels.hip: a workgroup's frames run two at a time with
+    their MB row pairs alternating, four LDS context slots; chosen for batches of one frame size with at
+    least two frames per workgroup, pick_chain_interleave): 549 distinct synthetic frames, so workgroups
+    hold two or three frames (an odd last frame runs alone); 176x80 has an odd MB row count (the last
+    pair of every frame is a single row).  Every slot against the oracle."""
+    import vp8g_batch
+    dev = torch.device("cuda:0")
+    n = 549
+    b = vp8g_batch.DeviceBatch(n, w, h, dev)
+    frames = [vp8g.synth_frame(w, h, 0x1A7E ^ i, profile=i % 3) for i in range(n)]
+    for i, f in enumerate(frames):
+        b.fill(i, f, bool(i % 5))
+    b.commit()
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    b.launch(stream)
+    torch.cuda.synchronize()
+    assert b.status_word() == 0
+    bad = [i for i, f in enumerate(frames) if b.frame_output(i) != vp8g.oracle_reconstruct(f, bool(i % 5))]
+    assert not bad, f"{len(bad)} of {n} slots differ, e.g. {bad[:8]}"
+    for f in frames:
+        f.free()

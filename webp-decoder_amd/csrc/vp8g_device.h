@@ -57,13 +57,18 @@ constexpr int kBpModes = 11;      // modes 0..9 + one constant-128 entry for out
 constexpr int kBpEntry = VP8G_BP_DCFOLD ? 32 : 16;  // bytes per (mode, pixel) entry
 constexpr int kDqTable = kBpTable + kBpModes * 16 * kBpEntry;  // 4 segments x 6 int16 dequant factors
 constexpr int kLfTable = kDqTable + 48;                 // 4 segments x 2 (B_PRED?) x {E, I, T, 0}
-constexpr int kTabStride = 80;                          // per frame slot (chain mode: two slots)
-constexpr int kMisc = kDqTable + 2 * kTabStride;        // chain mode: list length
+constexpr int kTabStride = 80;                          // per frame slot (chain mode: two slots, four interleaved)
+constexpr int kTabSlots = 4;
+constexpr int kMisc = kDqTable + kTabSlots * kTabStride;  // chain mode: list length
 #ifndef VP8G_PRED_ROLE  // whole-block predictor: lane roles from a per-lane LDS word pair (kRoleTab)
 #define VP8G_PRED_ROLE 1
 #endif
 constexpr int kRoleTab = kMisc + 16;                    // (VP8G_PRED_ROLE) 32 lanes x 8 B
-constexpr int kHdrBytes = kRoleTab + (VP8G_PRED_ROLE ? 256 : 0);
+#ifndef VP8G_SPLIT_PROG  // two progress words per wave: prediction context done / step done (kProgMid)
+#define VP8G_SPLIT_PROG 0
+#endif
+constexpr int kProgMid = kRoleTab + (VP8G_PRED_ROLE ? 256 : 0);  // (VP8G_SPLIT_PROG) 16 x u32
+constexpr int kHdrBytes = kProgMid + (VP8G_SPLIT_PROG ? 64 : 0);
 
 // Shared per-MB-column context (one frame per workgroup).
 constexpr int kCtxRecBytes = 32;   // unfiltered bottom row: Y 16, U 8, V 8 (intra prediction)
@@ -115,13 +120,15 @@ inline size_t lds_bytes(int waves, uint32_t ctx_cols, bool global_ctx) {
 constexpr int kChainWaves = VP8G_CHAIN_NW;
 constexpr bool kChainG = VP8G_CHAIN_G != 0;
 constexpr int kChainWgPerCu = VP8G_CHAIN_WPC;
-// LDS context area of a chain workgroup: the two context slots, or (global context) the cost sort's
-// scratch of kCostClasses + n_frames words
-inline size_t chain_ctx_lds(uint32_t ctx_cols, uint32_t n_frames) {
-	return kChainG ? ((size_t)4 * (kCostClasses + n_frames) + 15) & ~(size_t)15 : 2 * (size_t)ctx_cols * kCtxBytesPerCol;
+// LDS context area of a chain workgroup: the two context slots (four when two frames run
+// interleaved, see pick_chain_interleave), or (global context) the cost sort's scratch of
+// kCostClasses + n_frames words
+inline size_t chain_ctx_lds(uint32_t ctx_cols, uint32_t n_frames, bool il = false) {
+	return kChainG ? ((size_t)4 * (kCostClasses + n_frames) + 15) & ~(size_t)15
+	               : (il ? 4 : 2) * (size_t)ctx_cols * kCtxBytesPerCol;
 }
-inline size_t chain_lds_bytes(uint32_t ctx_cols, uint32_t list_max, uint32_t n_frames) {
-	return (size_t)kHdrBytes + (size_t)kChainWaves * kWaveBytes + chain_ctx_lds(ctx_cols, n_frames) + 4 * (size_t)list_max;
+inline size_t chain_lds_bytes(uint32_t ctx_cols, uint32_t list_max, uint32_t n_frames, bool il = false) {
+	return (size_t)kHdrBytes + (size_t)kChainWaves * kWaveBytes + chain_ctx_lds(ctx_cols, n_frames, il) + 4 * (size_t)list_max;
 }
 
 // Process-wide launch gate (vp8g_shim.hip).  Launch modes whose workgroups wait on each other across
@@ -180,11 +187,16 @@ uint32_t pick_chain(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint32_t ct
 // Mirror split of a chain launch (vp8g_kernels.hip, kSegTop): worth it for ordered batches of at most
 // two frames per workgroup (VP8G_SPLITCHAIN=0 / 1 forces it off / on), and the doubled list must fit.
 bool pick_chain_split(uint32_t n_frames, uint32_t ctx_cols, uint32_t workgroups, bool ordered);
+// Two-frame interleave of a chain launch (vp8g_kernels.hip): the frames of a workgroup's list run two
+// at a time with their MB row pairs alternating (the pair above is two global pairs back), which
+// halves the chain's fill and drain.  Needs every frame of the batch the same size, four context
+// slots in LDS and no mirror split (VP8G_CHAIN_IL=0 / 1 forces it off / on where it fits).
+bool pick_chain_interleave(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint32_t ctx_cols, uint32_t workgroups, bool split);
 // split: `snap` holds n_frames * ctx_cols * kCtxBytesPerCol bytes, `flags` n_frames words that hold
 // no value equal to `epoch` (a per-launch counter) before the launch.
 hipError_t launch_chain(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const Vp8gBatchArrays& arrays, uint8_t* d_out,
                         uint32_t ctx_cols, hipStream_t stream, uint32_t workgroups, bool ordered, bool split = false,
-                        uint8_t* snap = nullptr, uint32_t* flags = nullptr, uint32_t epoch = 0);
+                        uint8_t* snap = nullptr, uint32_t* flags = nullptr, uint32_t epoch = 0, bool interleave = false);
 
 constexpr uint32_t kMaxSplit = 8;
 int device_cus();

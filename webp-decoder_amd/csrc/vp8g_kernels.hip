@@ -75,7 +75,7 @@ constexpr int kPrioTab[11] = {VP8G_PRIO_TABLE, VP8G_PRIO_LF, VP8G_PRIO_WHT};
 #define VP8G_BP_REGION 1
 #endif
 #ifndef VP8G_PRED_FLAT  // whole-block predictor: DC sums without a branch, all loads in one round trip
-#define VP8G_PRED_FLAT 0
+#define VP8G_PRED_FLAT 1
 #endif
 #ifndef VP8G_DQ_B128  // residual: the dequant factors of all four segments in one 16-B LDS read
 #define VP8G_DQ_B128 1
@@ -83,6 +83,7 @@ constexpr int kPrioTab[11] = {VP8G_PRIO_TABLE, VP8G_PRIO_LF, VP8G_PRIO_WHT};
 #ifndef VP8G_LF_REDIRECT  // loop filter: stores without exec regions (chroma lanes' extra bytes to scratch)
 #define VP8G_LF_REDIRECT 0
 #endif
+static_assert(!VP8G_SPLIT_PROG || VP8G_FAST_STRIP, "the split progress path copies the filter state from kBorderTab roles");
 static_assert(!VP8G_LF_REDIRECT || VP8G_FAST_LF, "the store redirection's scratch bases come from the fast line addresses");
 #ifndef VP8G_LF_VPACK  // loop filter, vertical-edge pass: dword row gathers / scatters instead of byte accesses
 #define VP8G_LF_VPACK 0
@@ -792,7 +793,9 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 	const uint32_t slot_bytes = ctx_cols * (uint32_t)kCtxBytesPerCol;
 	uint8_t* const ctx_base = smem + kHdrBytes + NW * kWaveBytes;
 	// (kC) after the two context slots (global context: after the cost sort's scratch)
-	uint32_t* const chain_list = (uint32_t*)(ctx_base + (kG ? ((4u * (kCostClasses + n_chain) + 15u) & ~15u) : 2u * slot_bytes));
+	// (kC, ord_first bit 2: two frames interleaved, four context slots)
+	const bool il = kC && (ord_first & 4u) != 0;
+	uint32_t* const chain_list = (uint32_t*)(ctx_base + (kG ? ((4u * (kCostClasses + n_chain) + 15u) & ~15u) : (il ? 4u : 2u) * slot_bytes));
 	uint32_t m_chain = 1;  // (kC) frames in this workgroup's list
 	uint32_t f;
 	if constexpr (kC) {
@@ -882,6 +885,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 	};
 	if constexpr (!kC) put_tables(descs[f], 0u, (int)threadIdx.x);
 	if (threadIdx.x < 16) ((uint32_t*)(smem + kProgress))[threadIdx.x] = 0;
+	if (VP8G_SPLIT_PROG && threadIdx.x < 16) ((uint32_t*)(smem + kProgMid))[threadIdx.x] = 0;
 	__syncthreads();
 	if (kC && m_chain == 0) return;
 
@@ -913,6 +917,9 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 	set_frame(f, 0u);
 	uint32_t flags_l = flags;  // (laundered per step, VP8G_LAUNDER)
 	uint32_t* const prog = (uint32_t*)(smem + kProgress);
+	// (VP8G_SPLIT_PROG) a wave's progress after its prediction context (ctx_rec) is written: a successor's
+	// borders and prediction need only that; its loop filter waits for the full step (ctx_lf)
+	uint32_t* const progm = (uint32_t*)(smem + kProgMid);
 	const uint32_t GW = K * NW, gw = part * NW + (uint32_t)wave;
 	const size_t chan = (size_t)ctx_cols * kCtxBytesPerCol;
 	const uint32_t pin = (part + K - 1) % K;  // the part holding this part's wave-0 predecessors
@@ -951,11 +958,12 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 	// is garbage and the status word says so), so a stalled producer costs one bound, not one per step.
 	bool dead = false;
 	// bounded wait until the progress word of wave pw reaches `need`
-	auto wait_prog = [&](uint32_t pw, uint32_t need, bool xin_) {
+	auto wait_prog = [&](uint32_t pw, uint32_t need, bool xin_, uint32_t* pa = nullptr) {
 		uint32_t spins = 0;
 		uint64_t t0 = 0;
+		uint32_t* const pw_ = (pa ? pa : prog) + pw;
 		while (((kS && xin_) ? __hip_atomic_load(gp_in, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-		             : __hip_atomic_load(prog + pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < need) {
+		             : __hip_atomic_load(pw_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < need) {
 			__builtin_amdgcn_s_sleep(VP8G_WAIT_SLEEP);
 			if ((++spins & 1023u) == 0) {
 				const uint64_t now = __builtin_amdgcn_s_memrealtime();
@@ -1001,12 +1009,43 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 		return tag == 0u ? np : (tag == kSegTop ? (np + 1u) >> 1 : np >> 1);
 	};
 	uint32_t jf = 0, gbase = 0, ecur = kC ? uni(chain_list[0]) : f, np_c = kC ? seg_pairs(ecur) : npairs;
+	// (interleave) pairs per frame -- every frame of the batch has the same size
+	const uint32_t ilP = il ? uni(pairs_of(ecur & kSegMask)) : 0u;
 	for (uint32_t g = gw;; g += GW) {
 		uint32_t k;
 		bool has_pred;        // the pair above is decoded by this workgroup (else: frame top, or a bottom segment's snapshot)
 		bool snap_out = false;  // (kC) the top segment's last pair: context -> snapshot after its last step
 		uint32_t fcur = f;
-		if constexpr (kC) {
+		uint32_t dg = 1;      // global pairs back to the pair above (2 when two frames run interleaved)
+		if (il) {
+			// Two frames at a time: list entries 2m, 2m + 1 form group m, whose 2P global pairs alternate
+			// between them (pair k of frame 2m + e is global pair m * 2P + 2k + e, its pair above two
+			// global pairs back, i.e. two waves back); an odd last entry runs alone.  Frame j uses
+			// context slot j & 3: its first pair waits for frame j - 4's last pair.
+			const uint32_t gp = 2u * ilP, m = g / gp, off = g - m * gp;
+			if (m >= (m_chain >> 1)) {  // the odd tail frame, sequential
+				if (m > (m_chain >> 1) || !(m_chain & 1u) || off >= ilP) break;
+				jf = 2u * m, k = off, dg = 1u;
+			} else {
+				jf = 2u * m + (off & 1u), k = off >> 1, dg = 2u;
+			}
+			jf = uni(jf), k = uni(k), dg = uni(dg);
+			ecur = uni(chain_list[jf]);
+			fcur = ecur & kSegMask;
+			set_frame(fcur, jf & 3u);
+			has_pred = k > 0;
+			if (k == 0) {
+				if (jf >= 4u && !dead) {
+					const uint32_t j4 = jf - 4u, last4 = (j4 >> 1) * gp + 2u * (ilP - 1u) + (j4 & 1u);
+					const uint32_t T4 = 2u * (ilP - 1u) + 1u < R ? C + 2u : C;
+					wait_prog(last4 % NW, (last4 << kProgShift) + T4, false);
+				}
+				put_tables(*Dp, tabo, lane0);
+				wave_lds_sync();
+			} else if (!dead) {
+				wait_prog((uint32_t)((wave + NW - dg) % NW), ((g - dg) << kProgShift) + 1u, false);
+			}
+		} else if constexpr (kC) {
 			while (g >= gbase + np_c) {  // advance to the segment holding global pair g
 				gbase += np_c;
 				if (++jf >= m_chain) break;
@@ -1373,7 +1412,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 				const uint32_t lag = xin ? 5u : 4u;
 				const uint32_t ahead = (t + lag < CP2) ? t + lag : CP2;
 				if (xin) wait_prog(0u, (k - 1) * CP2 + ahead, true);
-				else wait_prog((uint32_t)((wave + NW - 1) % NW), ((g - 1u) << kProgShift) + ahead, false);
+				else wait_prog((uint32_t)((wave + NW - dg) % NW), ((g - dg) << kProgShift) + ahead, false, VP8G_SPLIT_PROG ? progm : prog);
 			}
 			if (kS && xin) {
 				// mailbox -> this part's LDS ctx: rec[t + 1] and lf[t] now (loaded last step; at t = 0
@@ -1440,7 +1479,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 					const uint32_t v = kind == 0 ? vabove : (kind == 1 ? 0x81818181u : vcorner);
 					if (ln < 20 && (kind != 1 || c == 0)) st32(hv + (bt & 0xFFFu), v);
 				}
-				if (lf_on && !top && ln >= 20) {  // filter state of the MB above (both modes; roles in kBorderTab)
+				if (!(VP8G_SPLIT_PROG && !xin) && lf_on && !top && ln >= 20) {  // filter state of the MB above (both modes; roles in kBorderTab)
 #if VP8G_FAST_STRIP
 					const uint32_t bt = bt_l;
 					const bool ly = (bt >> 22) & 1u;
@@ -1649,6 +1688,31 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 			// corner for the next MB is taken at its border setup)
 			STAMP(4);
 
+#if VP8G_SPLIT_PROG
+			// prediction context of this step is complete: successors may start their borders
+			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+			if (lane == 0 && wave != VP8G_TEST_STALL_WAVE)
+				__hip_atomic_store(progm + wave, (g << kProgShift) + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+			if (!xin) {
+				// the filter state of the MB above (ctx_lf) is written by the predecessor's flush: wait for
+				// its full step, then copy it into the tile's top rows (roles in kBorderTab)
+				PRIO(1);
+				if (has_pred && !dead && !(VP8G_ABLATE & 8)) {
+					const uint32_t ahead = (t + 4u < CP2) ? t + 4u : CP2;
+					wait_prog((uint32_t)((wave + NW - dg) % NW), ((g - dg) << kProgShift) + ahead, false, prog);
+				}
+				if (act && lf_on && r > 0 && ln >= 20) {
+					const uint32_t bt = bt_l;
+					const bool ly = (bt >> 22) & 1u;
+					const uint32_t lo = rec_off(cu) + ((bt >> 12) & 0xFFu);
+					uint8_t* const td = hv + (bt & 0xFFFu) + (slot ? (ly ? 16u : 8u) : 0u);
+					const u32x2 s0 = ctx.rd64(lo), s1 = ctx.rd64(lo + 8);
+					if (ly) st64(td, s0), st64(td + 8, s1);
+					else stc64(td, s0);
+				}
+				wave_lds_sync();
+			}
+#endif
 			// ---------------------------------------------- loop filter MB(r, c)
 			PRIO(5);
 			if (lf_on && !(VP8G_ABLATE & 1)) {
@@ -2052,13 +2116,29 @@ bool pick_chain_split(uint32_t n_frames, uint32_t ctx_cols, uint32_t workgroups,
 	return mode > 0 || (ordered && list_max <= 2);
 }
 
+bool pick_chain_interleave(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint32_t ctx_cols, uint32_t workgroups, bool split) {
+#ifndef VP8G_CHAIN_IL_DEFAULT  // (A/B builds: -DVP8G_CHAIN_IL_DEFAULT=0)
+#define VP8G_CHAIN_IL_DEFAULT -1
+#endif
+	static const int mode = [] {  // VP8G_CHAIN_IL=0: never, =1: wherever it fits (A/B experiments, tests)
+		const char* e = getenv("VP8G_CHAIN_IL");
+		return e ? atoi(e) : VP8G_CHAIN_IL_DEFAULT;
+	}();
+	if (mode == 0 || kChainG || split || workgroups == 0 || n_frames < 2 * workgroups) return false;
+	for (uint32_t i = 1; i < n_frames; i++)
+		if (h_descs[i].mb_cols != h_descs[0].mb_cols || h_descs[i].mb_rows != h_descs[0].mb_rows) return false;
+	if (h_descs[0].mb_rows < 2) return false;
+	const uint32_t list_max = (n_frames + workgroups - 1) / workgroups;
+	return (size_t)kChainWgPerCu * chain_lds_bytes(ctx_cols, list_max, n_frames, true) <= (size_t)kMaxLds;
+}
+
 hipError_t launch_chain(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const Vp8gBatchArrays& arrays, uint8_t* d_out,
                         uint32_t ctx_cols, hipStream_t stream, uint32_t workgroups, bool ordered, bool split, uint8_t* snap,
-                        uint32_t* flags, uint32_t epoch) {
+                        uint32_t* flags, uint32_t epoch, bool interleave) {
 	if (n_frames == 0) return hipSuccess;
-	if ((split && (!snap || !flags)) || (kChainG && !snap)) return hipErrorInvalidValue;
+	if ((split && (!snap || !flags)) || (kChainG && !snap) || (interleave && split)) return hipErrorInvalidValue;
 	const uint32_t list_max = (n_frames + workgroups - 1) / workgroups;
-	const size_t lds = chain_lds_bytes(ctx_cols, split ? 2 * list_max : list_max, n_frames);
+	const size_t lds = chain_lds_bytes(ctx_cols, split ? 2 * list_max : list_max, n_frames, interleave);
 	auto fn = frame_kernel<kChainWaves, kChainG, false, true>;
 	hipError_t e = lds_attr<kChainWaves, kChainG, false, true>();
 	if (e != hipSuccess) return e;
@@ -2067,7 +2147,7 @@ hipError_t launch_chain(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const V
 	// ord_first = ordered | split << 1)
 	hipLaunchKernelGGL(fn, dim3(workgroups), dim3(kChainWaves * 64), lds, stream, d_descs, arrays, d_out, ctx_cols,
 	                   split || kChainG ? snap : nullptr, split ? epoch : 1u, nullptr, split ? flags : nullptr,
-	                   (ordered ? 1u : 0u) | (split ? 2u : 0u), n_frames);
+	                   (ordered ? 1u : 0u) | (split ? 2u : 0u) | (interleave ? 4u : 0u), n_frames);
 	return hipGetLastError();
 }
 

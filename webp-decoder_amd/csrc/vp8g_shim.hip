@@ -401,8 +401,9 @@ int run_locked(DevState& g_dev, const std::vector<Vp8gFrameDesc>& descs, const V
 			HIP_TRY(hipMemsetAsync(g_dev.sflags, 0, g_dev.sflags_cap, s), "memset(flags)");
 		}
 		crossed = split;
+		const bool il = vp8g::pick_chain_interleave(descs.data(), n, max_cols, wg, split);  // (1080p batches: two frames interleaved)
 		HIP_TRY(vp8g::launch_chain((const Vp8gFrameDesc*)d_descs, n, arr, d_out, max_cols, s, wg, ordered, split, g_dev.snap,
-		                           (uint32_t*)g_dev.sflags, g_dev.epoch),
+		                           (uint32_t*)g_dev.sflags, g_dev.epoch, il),
 		        "launch");
 	} else {
 		const uint32_t ord = vp8g::pick_order(descs.data(), n, 1);  // cost-balanced placement (vp8g_device.h)
