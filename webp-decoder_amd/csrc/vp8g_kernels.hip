@@ -1019,15 +1019,18 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 		uint32_t dg = 1;      // global pairs back to the pair above (2 when two frames run interleaved)
 		if (il) {
 			// Two frames at a time: list entries 2m, 2m + 1 form group m, whose 2P global pairs alternate
-			// between them (pair k of frame 2m + e is global pair m * 2P + 2k + e, its pair above two
-			// global pairs back, i.e. two waves back); an odd last entry runs alone.  Frame j uses
-			// context slot j & 3: its first pair waits for frame j - 4's last pair.
+			// between them (pair k of frame 2m + e is global pair m * 2P + 2k + (e ^ (m & 1)), its pair
+			// above two global pairs back, i.e. two waves back); an odd last entry runs alone.  2P is even,
+			// so a wave keeps its parity's role in every group: the swap on odd groups hands the even and
+			// the odd waves the snake's heavy and light list positions in turn (without it the even waves
+			// took every heavy frame, fhd4 +8 %).  Frame j uses context slot j & 3: its first pair waits
+			// for frame j - 4's last pair.
 			const uint32_t gp = 2u * ilP, m = g / gp, off = g - m * gp;
 			if (m >= (m_chain >> 1)) {  // the odd tail frame, sequential
 				if (m > (m_chain >> 1) || !(m_chain & 1u) || off >= ilP) break;
 				jf = 2u * m, k = off, dg = 1u;
 			} else {
-				jf = 2u * m + (off & 1u), k = off >> 1, dg = 2u;
+				jf = 2u * m + ((off ^ m) & 1u), k = off >> 1, dg = 2u;
 			}
 			jf = uni(jf), k = uni(k), dg = uni(dg);
 			ecur = uni(chain_list[jf]);
@@ -1036,7 +1039,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 			has_pred = k > 0;
 			if (k == 0) {
 				if (jf >= 4u && !dead) {
-					const uint32_t j4 = jf - 4u, last4 = (j4 >> 1) * gp + 2u * (ilP - 1u) + (j4 & 1u);
+					const uint32_t j4 = jf - 4u, last4 = (j4 >> 1) * gp + 2u * (ilP - 1u) + ((j4 ^ (j4 >> 1)) & 1u);
 					const uint32_t T4 = 2u * (ilP - 1u) + 1u < R ? C + 2u : C;
 					wait_prog(last4 % NW, (last4 << kProgShift) + T4, false);
 				}
