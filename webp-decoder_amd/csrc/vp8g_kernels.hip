@@ -352,6 +352,15 @@ DEV uint32_t pack2(int a, int b) { return __builtin_amdgcn_perm((uint32_t)b, (ui
 DEV uint32_t mulhi2(uint32_t x, int c) {
 	return __builtin_amdgcn_perm((uint32_t)(hi_s16(x) * c), (uint32_t)(lo_s16(x) * c), 0x07060302u);
 }
+#ifndef VP8G_IDCT_MH  // iDCT row pass: the multiplies by v_mul_hi_i32 on the masked high half
+#define VP8G_IDCT_MH 0
+#endif
+// Row pass multiplies of the high int16 half h of a packed word w, from w & 0xFFFF0000 = h * 65536:
+// mul_s(h) = floor(h * 35468 / 65536) and mul_c(h) = h + floor(h * 20091 / 65536) =
+// floor(h * 85627 / 65536), one v_mul_hi_i32 each -- exact, and no extraction, shift or add of h
+DEV int mulhi32(int hx, int c) { return (int)(((long long)hx * c) >> 32); }
+DEV int mul_s_hi(uint32_t w) { return mulhi32((int)(w & 0xFFFF0000u), 35468); }
+DEV int mul_c_hi(uint32_t w) { return mulhi32((int)(w & 0xFFFF0000u), 85627); }
 DEV uint32_t mul_s2(uint32_t x) { return pk_add(x, mulhi2(x, 35468 - 65536)); }  // mul_s of both halves, mod 2^16
 DEV uint32_t mul_c2(uint32_t x) { return pk_add(x, mulhi2(x, 20091)); }
 // c ? a : b per lane, as two v_cndmask (opaque to the optimiser)
@@ -1360,8 +1369,12 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 					int c1[4], d1[4];
 #pragma unroll
 					for (int r = 0; r < 4; r++) {
+#if VP8G_IDCT_MH
+						c1[r] = mul_s_hi(oh[r]), d1[r] = mul_c_hi(oh[r]);
+#else
 						const int x1 = hi_s16(oh[r]);
 						c1[r] = mul_s(x1), d1[r] = mul_c(x1);
+#endif
 					}
 					const uint32_t dcadd = wht_dc();
 #pragma unroll
@@ -1385,8 +1398,12 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 					int c1[4], d1[4];
 #pragma unroll
 					for (int r = 0; r < 4; r++) {
+#if VP8G_IDCT_MH
+						c1[r] = mul_s_hi(o[2 * r]) - mul_c_hi(o[2 * r + 1]), d1[r] = mul_c_hi(o[2 * r]) + mul_s_hi(o[2 * r + 1]);
+#else
 						const int x1 = hi_s16(o[2 * r]), x3 = hi_s16(o[2 * r + 1]);
 						c1[r] = mul_s(x1) - mul_c(x3), d1[r] = mul_c(x1) + mul_s(x3);
+#endif
 					}
 					const uint32_t dcadd = wht_dc();
 #pragma unroll
