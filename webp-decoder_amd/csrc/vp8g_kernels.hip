@@ -388,8 +388,14 @@ DEV Rsrc plane_rsrc(uint8_t* base, uint32_t bytes) {
 	                    (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
 	return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)bu, (short)0, __builtin_amdgcn_readfirstlane((int)bytes), 0x00020000);
 }
-#ifndef VP8G_STORE_AUX  // cache-policy bits of the output pixel stores (A/B experiments)
-#define VP8G_STORE_AUX 0
+// Cache policy of the output pixel stores: sc1, write-through.  A 128-B output line collects its
+// 16-B (luma) / 8-B (chroma) row pieces over 8 / 16 MB steps; stored plainly, the partial lines sat
+// dirty in the XCD's L2 (4 MB: about the launch's whole in-flight set), were evicted half written
+// and refilled (3x the algorithmic write bytes).  sc1 stores leave L2 at once and
+// drop the line, so they neither occupy L2 nor need a refill (A/B uhd4 -1.5 %, fhd4 -2.4 %,
+// byte-identical; `nt` stores, which keep the line, were +120 %).
+#ifndef VP8G_STORE_AUX
+#define VP8G_STORE_AUX 16
 #endif
 constexpr int kCpolSc1 = 16;   // cache-policy bits of a buffer access: sc1 (device-coherent, bypasses the CU's L1)
 constexpr int kSnapBatch = 8;  // mirror split: 16-B snapshot loads per lane in flight
