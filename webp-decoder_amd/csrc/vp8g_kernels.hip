@@ -80,6 +80,9 @@ constexpr int kPrioTab[11] = {VP8G_PRIO_TABLE, VP8G_PRIO_LF, VP8G_PRIO_WHT};
 #ifndef VP8G_DQ_B128  // residual: the dequant factors of all four segments in one 16-B LDS read
 #define VP8G_DQ_B128 1
 #endif
+#ifndef VP8G_LOAD_NT  // (experiment) coefficient prefetch with the nt cache policy
+#define VP8G_LOAD_NT 0
+#endif
 #ifndef VP8G_LF_REDIRECT  // loop filter: stores without exec regions (chroma lanes' extra bytes to scratch)
 #define VP8G_LF_REDIRECT 0
 #endif
@@ -963,8 +966,13 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 		const gu32x4* src = (const gu32x4*)(cbase + ((uint64_t)cn << csh));
 		// (default cache policy: non-temporal loads measured 1 % slower and cost 11 % more HBM
 		// writes -- streamed coefficients then crowd out the partially written output lines in L2)
+#if VP8G_LOAD_NT  // (experiment: non-temporal coefficient loads)
+		p.a = __builtin_nontemporal_load(src);
+		p.b = __builtin_nontemporal_load(ln == 25 ? src : src + 1);
+#else
 		p.a = *src;
 		p.b = *(ln == 25 ? src : src + 1);
+#endif
 		p.side = ((const __attribute__((address_space(1))) uint8_t*)sbase)[cn];
 		return p;
 	};
