@@ -60,9 +60,10 @@ out = {
     "hbm_bytes_per_launch": round(read_b + write_b),
     "per_mb": {"read": round(read_b / mbs, 1), "write": round(write_b / mbs, 1),
                "algorithmic_read": 820, "algorithmic_write": 384},
-    "note": "FETCH_SIZE doubled (gfx950 tallies 128-B requests at 64 B); write amplification = "
-            "partial-line row pieces (16 B luma / 8 B chroma per row per MB) evicted before "
-            "their neighbours arrive",
+    "note": "FETCH_SIZE doubled (gfx950 tallies 128-B requests at 64 B). Writes: the output row "
+            "pieces are 16 B (luma) / 8 B (chroma) per row per MB; with write-through (sc1) stores "
+            "(round 4) each counts as one 32-B write (16 x 32 + 16 x 32 = 1024 B per MB); with plain "
+            "stores (up to r04d) partially written lines were evicted and refilled from HBM",
 }
 (prof / "traffic_4k_batch.json").write_text(json.dumps(out, indent=1) + "\n")
 print(json.dumps(out, indent=1))
