@@ -80,9 +80,6 @@ constexpr int kPrioTab[11] = {VP8G_PRIO_TABLE, VP8G_PRIO_LF, VP8G_PRIO_WHT};
 #ifndef VP8G_DQ_B128  // residual: the dequant factors of all four segments in one 16-B LDS read
 #define VP8G_DQ_B128 1
 #endif
-#ifndef VP8G_C16  // flush: chroma row pieces of two MB columns as one 16-B store (whole-piece frames)
-#define VP8G_C16 0
-#endif
 #ifndef VP8G_LOAD_NT  // (experiment) coefficient prefetch with the nt cache policy
 #define VP8G_LOAD_NT 0
 #endif
@@ -1185,12 +1182,6 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 #endif
 #if VP8G_FAST_FLUSH
 		const bool fl_fast = lf_on && W == 16u * C && ((yal | sy) & 15u) == 0 && ((ual | suv | vofs) & 7u) == 0;
-#if VP8G_C16
-		// chroma pairs: an even column's 8-B piece is held one step and stored with the odd column's
-		// as one 16-B store (16-B aligned rows, an even column count so every even column has a partner)
-		const bool c16 = fl_fast && ((ual | suv | vofs) & 15u) == 0 && (C & 1u) == 0;
-		u32x2 c16prev = u32x2{0u, 0u};
-#endif
 #endif
 		{
 			const int hh = lane0 >> 5, ln = lane0 & 31;
@@ -1827,10 +1818,6 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 			// visible but cut by the right edge, or not aligned, goes byte by byte (rare branch).
 			uint32_t offY = kNoStore, offC = kNoStore, poffY = 0, poffC = 0, pcntY = 0, pcntC = 0;
 			u32x2 yl0, yl1, cl0;
-#if VP8G_C16
-			uint32_t off16 = kNoStore;
-			u32x4 d16 = u32x4{0u, 0u, 0u, 0u};
-#endif
 			const uint8_t* srcY;
 			const uint8_t* srcC;
 			if (!lf_on) {
@@ -1876,18 +1863,6 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 				cl0 = ldc64(srcC);
 				if (okcc && (int)lcx > 0x3FFFFFFF) ctx.wr64(lcx + (t160 - 0x40000000u), cl0);
 				offC = okcc ? fl_offC + t * 8u : kNoStore;
-#if VP8G_C16
-				if (c16) {
-					// odd column: {held even piece, this piece} as one store at the even column's offset; a
-					// left-MB lane at the frame's last column stores its (even) column C - 2 alone, 8 B
-					const bool lastl = kr >= 4 && cu + 1u == C;
-					const bool oddc = (((ual + offC) >> 3) & 1u) != 0u;
-					off16 = oddc && offC != kNoStore ? offC - 8u : kNoStore;
-					d16 = u32x4{c16prev.x, c16prev.y, cl0.x, cl0.y};
-					c16prev = cl0;
-					offC = lastl ? offC : kNoStore;
-				}
-#endif
 #if VP8G_ABLATE & 16
 				// diagnostic (output wrong): the same stores of the same lanes, linearised per wave half, so
 				// each step's pieces fill whole consecutive lines -- the traffic and time without partial lines
@@ -1942,9 +1917,6 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 				}
 			}
 			bst128(rY, offY, u32x4{yl0.x, yl0.y, yl1.x, yl1.y});
-#if VP8G_C16
-			bst128(rC, off16, d16);
-#endif
 			bst64(rC, offC, cl0);
 			if (__ballot(pcntY | pcntC) != 0ull) {
 				for (uint32_t q = 0; q < pcntY; q++) outY[poffY + q] = srcY[q];
