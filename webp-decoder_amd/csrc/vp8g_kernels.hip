@@ -80,6 +80,9 @@ constexpr int kPrioTab[11] = {VP8G_PRIO_TABLE, VP8G_PRIO_LF, VP8G_PRIO_WHT};
 #ifndef VP8G_DQ_B128  // residual: the dequant factors of all four segments in one 16-B LDS read
 #define VP8G_DQ_B128 1
 #endif
+#ifndef VP8G_WHT_LOCAL  // iWHT: both passes in the Y2 lanes without an LDS round trip between them
+#define VP8G_WHT_LOCAL 0
+#endif
 #ifndef VP8G_LOAD_NT  // (experiment) coefficient prefetch with the nt cache policy
 #define VP8G_LOAD_NT 0
 #endif
@@ -1328,6 +1331,27 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 				if (__ballot(act && !bpred) != 0ull) {
 					PRIO(10);
 					const bool wl = ln >= 26 && ln < 30;
+#if VP8G_WHT_LOCAL
+					// every WHT lane holds the whole Y2 block: it runs the vertical pass of both column pairs
+					// itself and keeps its own row (ln - 26) -- no LDS round trip between the passes
+					if (wl) {
+						uint32_t v[8];
+#pragma unroll
+						for (int h = 0; h < 2; h++) {
+							const uint32_t a1 = pk_add(w[h], w[6 + h]), b1 = pk_add(w[2 + h], w[4 + h]);
+							const uint32_t c1 = pk_sub(w[2 + h], w[4 + h]), d1 = pk_sub(w[h], w[6 + h]);
+							v[h] = pk_add(a1, b1), v[2 + h] = pk_add(c1, d1), v[4 + h] = pk_sub(a1, b1), v[6 + h] = pk_sub(d1, c1);
+						}
+						const bool r1 = ((ln - 26) & 1) != 0, r2 = ((ln - 26) & 2) != 0;
+						const uint32_t tx = r2 ? (r1 ? v[6] : v[4]) : (r1 ? v[2] : v[0]);
+						const uint32_t ty = r2 ? (r1 ? v[7] : v[5]) : (r1 ? v[3] : v[1]);
+						uint8_t* const q = hv + kWht + 8 * (ln - 26);
+						const int q0 = lo_s16(tx), q1 = hi_s16(tx), q2 = lo_s16(ty), q3 = hi_s16(ty);
+						const int a1 = q0 + q3 + 3, b1 = q1 + q2, c1 = q1 - q2, d1 = q0 - q3 + 3;
+						st64(q, u32x2{pack2((a1 + b1) >> 3, (c1 + d1) >> 3), pack2((a1 - b1) >> 3, (d1 - c1) >> 3)});
+					}
+					if (false) {
+#endif
 					{
 						const int h = ln & 1;
 						const uint32_t r0 = h ? w[1] : w[0], r1 = h ? w[3] : w[2], r2 = h ? w[5] : w[4], r3 = h ? w[7] : w[6];
@@ -1348,6 +1372,9 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 						const int a1 = q0 + q3 + 3, b1 = q1 + q2, c1 = q1 - q2, d1 = q0 - q3 + 3;
 						st64(q, u32x2{pack2((a1 + b1) >> 3, (c1 + d1) >> 3), pack2((a1 - b1) >> 3, (d1 - c1) >> 3)});
 					}
+#if VP8G_WHT_LOCAL
+					}
+#endif
 					wave_lds_sync();
 					if (ln < 16 && !bpred) w[0] = (w[0] & 0xFFFF0000u) | *(const uint16_t*)(hv + kWht + 2 * ln);
 					PRIO(0);
