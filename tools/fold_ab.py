@@ -2,13 +2,13 @@
 """Fold the summary lines of in-process A/B runs (gpurun_out/ab_<tag>/<workload>.jsonl, written by
 tools/gpu_round.sh ab) into one committed JSON file under profiles/.
 
-Usage: tools/fold_ab.py out.json tag=description [tag=description ...]
+Usage: tools/fold_ab.py out.json tag=description [tag=description ...]   (merges into out.json)
 """
 import json, os, sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 out, pairs = sys.argv[1], sys.argv[2:]
-res = {}
+res = json.load(open(out)) if os.path.exists(out) else {}  # (tags already folded are kept or replaced)
 for p in pairs:
     tag, _, what = p.partition("=")
     d = os.path.join(ROOT, "gpurun_out", "ab_" + tag)
