@@ -51,24 +51,14 @@ constexpr int kProgress = 0;      // 16 x u32 progress words (one per wave)
 constexpr int kBpTable = 64;      // B_PRED predictor table: 11 modes x 16 px x {perm selectors, byte
                                   // mask, dot weights, bias | shift}
 constexpr int kBpModes = 11;      // modes 0..9 + one constant-128 entry for out-of-range modes
-#ifndef VP8G_BP_DCFOLD  // B_PRED: DC_PRED folded into the table's dot product (32-B entries)
-#define VP8G_BP_DCFOLD 0
-#endif
-constexpr int kBpEntry = VP8G_BP_DCFOLD ? 32 : 16;  // bytes per (mode, pixel) entry
+constexpr int kBpEntry = 16;      // bytes per (mode, pixel) entry
 constexpr int kDqTable = kBpTable + kBpModes * 16 * kBpEntry;  // 4 segments x 6 int16 dequant factors
 constexpr int kLfTable = kDqTable + 48;                 // 4 segments x 2 (B_PRED?) x {E, I, T, 0}
 constexpr int kTabStride = 80;                          // per frame slot (chain mode: two slots, four interleaved)
 constexpr int kTabSlots = 4;
 constexpr int kMisc = kDqTable + kTabSlots * kTabStride;  // chain mode: list length
-#ifndef VP8G_PRED_ROLE  // whole-block predictor: lane roles from a per-lane LDS word pair (kRoleTab)
-#define VP8G_PRED_ROLE 1
-#endif
-constexpr int kRoleTab = kMisc + 16;                    // (VP8G_PRED_ROLE) 32 lanes x 8 B
-#ifndef VP8G_SPLIT_PROG  // two progress words per wave: prediction context done / step done (kProgMid)
-#define VP8G_SPLIT_PROG 0
-#endif
-constexpr int kProgMid = kRoleTab + (VP8G_PRED_ROLE ? 256 : 0);  // (VP8G_SPLIT_PROG) 16 x u32
-constexpr int kHdrBytes = kProgMid + (VP8G_SPLIT_PROG ? 64 : 0);
+constexpr int kRoleTab = kMisc + 16;                    // whole-block predictor lane roles: 32 lanes x 8 B
+constexpr int kHdrBytes = kRoleTab + 256;
 
 // Shared per-MB-column context (one frame per workgroup).
 constexpr int kCtxRecBytes = 32;   // unfiltered bottom row: Y 16, U 8, V 8 (intra prediction)

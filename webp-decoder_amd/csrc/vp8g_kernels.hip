@@ -53,53 +53,8 @@ constexpr int kPrioTab[11] = {VP8G_PRIO_TABLE, VP8G_PRIO_LF, VP8G_PRIO_WHT};
 #ifndef VP8G_ABLATE
 #define VP8G_ABLATE 0
 #endif
-#ifndef VP8G_LAUNDER  // step loop: invariant per-lane words and frame flags re-laundered every step
-#define VP8G_LAUNDER 1
-#endif
-#ifndef VP8G_FAST_FLUSH  // flush: per-pair folded store offsets for whole-piece frames (fl_fast)
-#define VP8G_FAST_FLUSH 1
-#endif
-#ifndef VP8G_FAST_STRIP  // borders: the filter-state copy of lanes 20..31 from kBorderTab roles
-#define VP8G_FAST_STRIP 1
-#endif
-#ifndef VP8G_IDCT_C01  // iDCT: a cheaper transform when columns 2 and 3 of every block of the wave are zero
-#define VP8G_IDCT_C01 1
-#endif
-#ifndef VP8G_KATTR  // (experiments: e.g. __attribute__((amdgpu_num_vgpr(112))) to probe the register budget)
-#define VP8G_KATTR
-#endif
-#ifndef VP8G_FAST_LF  // loop filter: line addresses from per-pair lane words (lf_vp / lf_hp)
-#define VP8G_FAST_LF 1
-#endif
-#ifndef VP8G_BP_REGION  // B_PRED: one exec region around the wavefront instead of one per step
-#define VP8G_BP_REGION 1
-#endif
-#ifndef VP8G_PRED_FLAT  // whole-block predictor: DC sums without a branch, all loads in one round trip
-#define VP8G_PRED_FLAT 1
-#endif
-#ifndef VP8G_DQ_B128  // residual: the dequant factors of all four segments in one 16-B LDS read
-#define VP8G_DQ_B128 1
-#endif
-#ifndef VP8G_WHT_LOCAL  // iWHT: both passes in the Y2 lanes without an LDS round trip between them
-#define VP8G_WHT_LOCAL 0
-#endif
-#ifndef VP8G_LOAD_NT  // (experiment) coefficient prefetch with the nt cache policy
-#define VP8G_LOAD_NT 0
-#endif
-#ifndef VP8G_LF_REDIRECT  // loop filter: stores without exec regions (chroma lanes' extra bytes to scratch)
-#define VP8G_LF_REDIRECT 0
-#endif
-static_assert(!VP8G_SPLIT_PROG || VP8G_FAST_STRIP, "the split progress path copies the filter state from kBorderTab roles");
-static_assert(!VP8G_LF_REDIRECT || VP8G_FAST_LF, "the store redirection's scratch bases come from the fast line addresses");
-#ifndef VP8G_LF_VPACK  // loop filter, vertical-edge pass: dword row gathers / scatters instead of byte accesses
-#define VP8G_LF_VPACK 0
-#endif
-#ifndef VP8G_LF_VSTORE  // loop filter, vertical-edge pass: write-back as dwords (byte gathers kept)
-#define VP8G_LF_VSTORE 1
-#endif
-#ifndef VP8G_LF_SELECT  // loop filter: masked filter input by select instead of a branch (sel0)
-#define VP8G_LF_SELECT 0
-#endif
+// (Rejected experiments -- their numbers are in DESIGN.md §6 -- were removed in round 5; the shipped
+// paths are unconditional now.  The remaining switches are the diagnostics above and below.)
 // Bound of one dependency wait in s_memrealtime ticks (100 MHz): 2 s.  Test builds shorten it and
 // make one wave never publish its progress (VP8G_TEST_STALL_WAVE) to check that a stalled producer
 // ends the launch promptly with VP8G_ERR_TIMEOUT (tests/test_gpu_batch.py).
@@ -203,25 +158,10 @@ constexpr BpTab make_bptab() {
 			// weights (signed bytes) and bias / shift of the one dot-product formula:
 			// value = (sdot4(E_xyz - 128, w) + bias) >> sh  (avg3: (1, 2, 1), 514, 2; TM: (1, -1, 1), 128, 0)
 			const bool tm = m == 1;
-#if VP8G_BP_DCFOLD
-			// 32-B entry {sel, byte mask, weights, bias, shift, above-row mask, 0, 0}: DC_PRED is the dot
-			// of the four left bytes (selectors 0..3, weights 1) plus a v_sad_u8 of the four above bytes
-			// under the above-row mask, (sum + 4) >> 3; every other mode masks the above row to zero
-			const bool dc = m == 0;
-			uint32_t* const en = &t.v[(m * 16 + p) * 8];
-			en[0] = dc ? 0x03020100u : sel;
-			en[1] = dc ? 0u : mask;
-			en[2] = dc ? 0x01010101u : (tm ? 0x0001FF01u : 0x00010201u);
-			en[3] = dc ? 516u : (tm ? 128u : 514u);
-			en[4] = dc ? 3u : (tm ? 0u : 2u);
-			en[5] = dc ? 0xFFFFFFFFu : 0u;
-			en[6] = en[7] = 0u;
-#else
 			t.v[(m * 16 + p) * 4] = sel;
 			t.v[(m * 16 + p) * 4 + 1] = mask | ((tm ? 0u : 2u) << 24);  // byte 3: the shift (x3's byte 3 is unused)
 			t.v[(m * 16 + p) * 4 + 2] = tm ? 0x0001FF01u : 0x00010201u;
 			t.v[(m * 16 + p) * 4 + 3] = tm ? 128u : 514u;
-#endif
 		}
 	return t;
 }
@@ -258,7 +198,7 @@ constexpr BorderTab make_bordertab() {
 }
 __constant__ BorderTab kBorderTab = make_bordertab();
 
-// Whole-block predictor roles of lanes 0..23 (VP8G_PRED_ROLE; offsets from the half's area):
+// Whole-block predictor roles of lanes 0..23 (offsets from the half's area):
 // v[2 ln] = above-row base | own above word << 11 | is-luma << 22 | last block row << 23 | last
 // block column << 24 | offset in the ctx_rec column << 25; v[2 ln + 1] = left-column base |
 // destination in the tile at slot 0 << 11 | block row << 22.
@@ -360,9 +300,6 @@ DEV uint32_t sat_pk(uint32_t x) {
 	asm("v_sat_pk_u8_i16 %0, %1" : "=v"(r) : "v"(x));
 	return r;
 }
-#ifndef VP8G_SATPK
-#define VP8G_SATPK 1
-#endif
 DEV int lo_s16(uint32_t x) { return (int)(int16_t)(x & 0xFFFFu); }
 DEV int hi_s16(uint32_t x) { return (int)(int16_t)(x >> 16); }
 DEV uint32_t pack2(int a, int b) { return __builtin_amdgcn_perm((uint32_t)b, (uint32_t)a, 0x05040100u); }
@@ -370,15 +307,6 @@ DEV uint32_t pack2(int a, int b) { return __builtin_amdgcn_perm((uint32_t)b, (ui
 DEV uint32_t mulhi2(uint32_t x, int c) {
 	return __builtin_amdgcn_perm((uint32_t)(hi_s16(x) * c), (uint32_t)(lo_s16(x) * c), 0x07060302u);
 }
-#ifndef VP8G_IDCT_MH  // iDCT row pass: the multiplies by v_mul_hi_i32 on the masked high half
-#define VP8G_IDCT_MH 0
-#endif
-// Row pass multiplies of the high int16 half h of a packed word w, from w & 0xFFFF0000 = h * 65536:
-// mul_s(h) = floor(h * 35468 / 65536) and mul_c(h) = h + floor(h * 20091 / 65536) =
-// floor(h * 85627 / 65536), one v_mul_hi_i32 each -- exact, and no extraction, shift or add of h
-DEV int mulhi32(int hx, int c) { return (int)(((long long)hx * c) >> 32); }
-DEV int mul_s_hi(uint32_t w) { return mulhi32((int)(w & 0xFFFF0000u), 35468); }
-DEV int mul_c_hi(uint32_t w) { return mulhi32((int)(w & 0xFFFF0000u), 85627); }
 DEV uint32_t mul_s2(uint32_t x) { return pk_add(x, mulhi2(x, 35468 - 65536)); }  // mul_s of both halves, mod 2^16
 DEV uint32_t mul_c2(uint32_t x) { return pk_add(x, mulhi2(x, 20091)); }
 // c ? a : b per lane, as two v_cndmask (opaque to the optimiser)
@@ -483,18 +411,9 @@ DEV void edge_mask(const int* x, bool en, int lim, int I, int T, bool& m, bool& 
 	hev = hm > T;
 }
 
-// m ? v : 0 as one v_cndmask (opaque to the optimiser, which otherwise turns the select into an
-// exec-masked branch around the filter arithmetic: cheaper for frames whose edges mostly fail the
-// masks, dearer for the frames that filter most edges -- and those set the launch time)
-DEV int sel0(bool m, int v) {
-#if VP8G_LF_SELECT
-	int r;
-	asm volatile("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(r) : "v"(v), "s"(__builtin_amdgcn_ballot_w64(m)));
-	return r;
-#else
-	return m ? v : 0;
-#endif
-}
+// m ? v : 0 (the compiler makes it an exec-masked branch around the filter arithmetic; a forced
+// v_cndmask select measured +0.5...+1.8 %)
+DEV int sel0(bool m, int v) { return m ? v : 0; }
 
 // Masking: the filter input (the common-adjust value) is zeroed where the edge mask is off, which
 // makes every tap 0 ((0 + 4) >> 3 = (0 + 3) >> 3 = (0 + 63) >> 7 = 0), so one select per edge
@@ -604,17 +523,7 @@ struct LfLine {
 	uint8_t* Lp;
 	uint8_t* Mp;
 	uint8_t* colp;
-	uint8_t* Mhi;    // (VP8G_LF_REDIRECT) base of a lane's row bytes 10..17: Mp, or scratch for chroma lanes
-	uint8_t* colhi;  // (VP8G_LF_REDIRECT) base of a lane's column bytes 10..17: colp, or scratch for chroma
 };
-DEV LfLine lf_lines(uint8_t* tY, uint8_t* tC, int ln, int slot) {
-	const bool isy = ln < 16;
-	const int cp = (ln >> 3) & 1;
-	uint8_t* const rowp = isy ? tY + (4 + ln) * kTP : tC + (4 + (ln & 7)) * kTP + cp * kCV;
-	const int off = isy ? slot * 16 : slot * 8, ring = isy ? 31 : 15;
-	uint8_t* const colp = isy ? tY + slot * 16 + ln : tC + cp * kCV + slot * 8 + (ln & 7);
-	return LfLine{rowp + ((off - 4) & ring), rowp + off, colp, rowp + off, colp};
-}
 template <bool kSimple>
 DEV void lf_mb(const LfLine& L, int ln, bool en, bool mb_v, bool mb_h, bool inner, int E, int I, int T) {
 	const bool isy = ln < 16;
@@ -628,35 +537,11 @@ DEV void lf_mb(const LfLine& L, int ln, bool en, bool mb_v, bool mb_h, bool inne
 		uint8_t* const Lp = L.Lp;
 		uint8_t* const Mp = L.Mp;
 		PRIO(8);
-#if VP8G_LF_VPACK
-		// (experiment) the row as five dwords -- the left neighbour's 4 bytes and this MB's 16 (chroma:
-		// its 8 and 8 unused) -- unpacked with bit-field extracts, written back as packed dwords: 4 to 7
-		// LDS instructions instead of 37 byte accesses, for ~35 more vector instructions
-		{
-			const uint32_t w0 = ld32(Lp), w1 = ld32(Mp), w2 = ld32(Mp + 4), w3 = ld32(Mp + 8), w4 = ld32(Mp + 12);
-			const uint32_t wv[5] = {w0, w1, w2, w3, w4};
-#pragma unroll
-			for (int i = 0; i < 20; i++) px[i] = (int)__builtin_amdgcn_ubfe(wv[i >> 2], 8u * (uint32_t)(i & 3), 8u);
-		}
-		PRIO(9);
-		lf_line<kSimple>(px, en && mb_v, en && inner, isy, E, I, T);
-		if (wr) {
-			st32(Lp, pack4b(px[0], px[1], px[2], px[3]));
-			st32(Mp, pack4b(px[4], px[5], px[6], px[7]));
-			st32(Mp + 4, pack4b(px[8], px[9], px[10], px[11]));
-			if (isy) {
-				st32(Mp + 8, pack4b(px[12], px[13], px[14], px[15]));
-				st32(Mp + 12, pack4b(px[16], px[17], px[18], px[19]));
-			}
-		}
-		if (false) {
-#else
 		gather20<1, 1>(Lp, Mp, px);
 		PRIO(9);
 		lf_line<kSimple>(px, en && mb_v, en && inner, isy, E, I, T);
-#if VP8G_LF_VSTORE
-		// (experiment) the row written back as dwords -- bytes the filter leaves alone are rewritten
-		// unchanged; 3 / 5 LDS stores instead of 9 / 17 byte stores, for ~15 packing instructions
+		// the row written back as dwords -- bytes the filter leaves alone are rewritten unchanged;
+		// 3 / 5 LDS stores instead of 9 / 17 byte stores, for ~15 packing instructions
 		if (wr) {
 			st32(Lp, pack4b(px[0], px[1], px[2], px[3]));
 			st32(Mp, pack4b(px[4], px[5], px[6], px[7]));
@@ -665,27 +550,6 @@ DEV void lf_mb(const LfLine& L, int ln, bool en, bool mb_v, bool mb_h, bool inne
 				st32(Mp + 8, pack4b(px[12], px[13], px[14], px[15]));
 				st32(Mp + 12, pack4b(px[16], px[17], px[18], px[19]));
 			}
-		}
-		if (false) {
-#else
-		if (VP8G_LF_REDIRECT || wr) {
-#endif
-#endif
-#pragma unroll
-			for (int i = 1; i < 4; i++) stb(Lp + i, px[i]);
-#pragma unroll
-			for (int i = 0; i < 6; i++) stb(Mp + i, px[4 + i]);
-#if VP8G_LF_REDIRECT
-			// (no exec regions: a lane that filters nothing writes its unchanged bytes back, and the
-			// chroma lanes' bytes past their 8-pixel row go to scratch)
-#pragma unroll
-			for (int i = 6; i < 14; i++) stb(L.Mhi + i, px[4 + i]);
-#else
-			if (isy) {
-#pragma unroll
-				for (int i = 6; i < 14; i++) stb(Mp + i, px[4 + i]);
-			}
-#endif
 		}
 	}
 	wave_lds_sync();
@@ -696,18 +560,13 @@ DEV void lf_mb(const LfLine& L, int ln, bool en, bool mb_v, bool mb_h, bool inne
 		gather20<kTP, kTP>(colp, colp + 4 * kTP, px);
 		PRIO(9);
 		lf_line<kSimple>(px, en && mb_h, en && inner, isy, E, I, T);
-		if (VP8G_LF_REDIRECT || wr) {
+		if (wr) {
 #pragma unroll
 			for (int i = 1; i < 10; i++) stb(colp + kTP * i, px[i]);
-#if VP8G_LF_REDIRECT
-#pragma unroll
-			for (int i = 10; i < 18; i++) stb(L.colhi + kTP * i, px[i]);
-#else
 			if (isy) {
 #pragma unroll
 				for (int i = 10; i < 18; i++) stb(colp + kTP * i, px[i]);
 			}
-#endif
 		}
 	}
 	wave_lds_sync();
@@ -725,18 +584,9 @@ struct Pref {
 // Occupancy target: two workgroups (frames) per CU at NW <= 8 (2*NW waves per CU); one
 // workgroup of 12 or 16 waves per CU for batches smaller than the CU count (pick_waves).  Either
 // way at most 4 waves per SIMD, i.e. the full 128-VGPR budget.
-#ifndef VP8G_WPS8  // (experiments: waves per SIMD the 8-wave kernel is compiled for -- 6 = 80 VGPRs, three frames per CU)
-#define VP8G_WPS8 4
-#endif
-#ifndef VP8G_WPS16  // (experiments: the chain kernel's waves per SIMD; above 4 needs two workgroups per CU)
-#define VP8G_WPS16 4
-#endif
-#ifndef VP8G_WPS12  // (experiments: the 12-wave kernel at 6 waves per SIMD = 80 VGPRs, two frames per CU)
-#define VP8G_WPS12 4
-#endif
 template <int NW>
 constexpr int min_waves_per_simd() {
-	return NW == 10 ? 5 : (NW == 16 ? VP8G_WPS16 : NW == 8 ? VP8G_WPS8 : (NW == 12 ? VP8G_WPS12 : (NW >= 6 ? 4 : (NW >= 2 ? (2 * NW) / 4 : 1))));
+	return NW >= 6 ? 4 : (NW >= 2 ? (2 * NW) / 4 : 1);
 }
 
 // Split mode (kS, small batches): a frame's MB row pairs are dealt over `nsplit` workgroups
@@ -827,7 +677,7 @@ constexpr uint32_t kProgShift = 11;
 constexpr uint32_t kSegTop = 1u, kSegBottom = 2u, kSegMask = 0x3FFFFFFFu;  // list entry: frame | tag << 30
 
 template <int NW, bool kG, bool kS, bool kC>
-__global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void frame_kernel(const Vp8gFrameDesc* __restrict__ descs, Vp8gBatchArrays A,
+__global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kernel(const Vp8gFrameDesc* __restrict__ descs, Vp8gBatchArrays A,
                                                         uint8_t* __restrict__ out, uint32_t ctx_cols,
                                                         uint8_t* __restrict__ gctx, uint32_t nsplit,
                                                         uint8_t* __restrict__ mbox, uint32_t* __restrict__ gprog,
@@ -917,23 +767,20 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 	const uint32_t part = kS ? blockIdx.x / nfr : 0u;
 
 	for (int i = (int)threadIdx.x; i < kBpModes * 16 * (kBpEntry / 4); i += NW * 64) ((uint32_t*)(smem + kBpTable))[i] = kBpTab.v[i];
-#if VP8G_PRED_ROLE
 	if (threadIdx.x < 64) ((uint32_t*)(smem + kRoleTab))[threadIdx.x] = kPredRoleTab.v[threadIdx.x];
-#endif
 	uint32_t bt_l = kBorderTab.v[lane0 & 31];  // this lane's border-setup role (loop-invariant)
 	// dequant / loop-filter tables of a frame into its slot (chain mode: by the wave of the frame's pair 0)
 	auto put_tables = [&](const Vp8gFrameDesc& Df, uint32_t tabo, int l) {
-		// dequant factors as (dc, ac) int16 pairs, [class][segment] (VP8G_DQ_B128: one 16-B read per lane
-		// fetches a class's four segments before the segment is known) or [segment][class]
+		// dequant factors as (dc, ac) int16 pairs, [class][segment] (one 16-B read per lane
+		// fetches a class's four segments before the segment is known)
 		if (l < 24) {
 			const int sg = l / 6, k = l % 6, cl = k >> 1;
-			((int16_t*)(smem + kDqTable + tabo))[VP8G_DQ_B128 ? (cl * 4 + sg) * 2 + (k & 1) : l] = Df.dq[sg][k];
+			((int16_t*)(smem + kDqTable + tabo))[(cl * 4 + sg) * 2 + (k & 1)] = Df.dq[sg][k];
 		}
 		if (l < 32) smem[kLfTable + tabo + l] = Df.lf[l >> 3][(l >> 2) & 1][l & 3];
 	};
 	if constexpr (!kC) put_tables(descs[f], 0u, (int)threadIdx.x);
 	if (threadIdx.x < 16) ((uint32_t*)(smem + kProgress))[threadIdx.x] = 0;
-	if (VP8G_SPLIT_PROG && threadIdx.x < 16) ((uint32_t*)(smem + kProgMid))[threadIdx.x] = 0;
 	__syncthreads();
 	if (kC && m_chain == 0) return;
 
@@ -963,11 +810,8 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 		tabo = slot * (uint32_t)kTabStride;
 	};
 	set_frame(f, 0u);
-	uint32_t flags_l = flags;  // (laundered per step, VP8G_LAUNDER)
+	uint32_t flags_l = flags;  // (laundered per step)
 	uint32_t* const prog = (uint32_t*)(smem + kProgress);
-	// (VP8G_SPLIT_PROG) a wave's progress after its prediction context (ctx_rec) is written: a successor's
-	// borders and prediction need only that; its loop filter waits for the full step (ctx_lf)
-	uint32_t* const progm = (uint32_t*)(smem + kProgMid);
 	const uint32_t GW = K * NW, gw = part * NW + (uint32_t)wave;
 	const size_t chan = (size_t)ctx_cols * kCtxBytesPerCol;
 	const uint32_t pin = (part + K - 1) % K;  // the part holding this part's wave-0 predecessors
@@ -996,13 +840,8 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 		const gu32x4* src = (const gu32x4*)(cbase + ((uint64_t)cn << csh));
 		// (default cache policy: non-temporal loads measured 1 % slower and cost 11 % more HBM
 		// writes -- streamed coefficients then crowd out the partially written output lines in L2)
-#if VP8G_LOAD_NT  // (experiment: non-temporal coefficient loads)
-		p.a = __builtin_nontemporal_load(src);
-		p.b = __builtin_nontemporal_load(ln == 25 ? src : src + 1);
-#else
 		p.a = *src;
 		p.b = *(ln == 25 ? src : src + 1);
-#endif
 		p.side = ((const __attribute__((address_space(1))) uint8_t*)sbase)[cn];
 		return p;
 	};
@@ -1195,9 +1034,8 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 		// luma tile row ln (0..19) and chroma plane ln / 12, tile row ln % 12 of some column;
 		// image row = MB row origin + tile row - 4 (negative rows wrap and fail the crop test).
 		uint32_t fl_offY, fl_offC, fl_bits, fl_srcY = 0u, fl_srcC = 0u;
-#if VP8G_FAST_LF
-		// loop-filter line addresses of this lane (see lf_lines), relative to the wave's LDS area:
-		// slot 0 in bits 0..15, slot 1 in 16..31
+		// loop-filter line addresses of this lane (rows for the vertical-edge pass, columns for the
+		// horizontal-edge pass), relative to the wave's LDS area: slot 0 in bits 0..15, slot 1 in 16..31
 		uint32_t lf_vp, lf_hp;
 		{
 			const int hh = lane0 >> 5, ln = lane0 & 31;
@@ -1209,10 +1047,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 			lf_vp = rowp | ((rowp + d) << 16);
 			lf_hp = col | ((col + d) << 16);
 		}
-#endif
-#if VP8G_FAST_FLUSH
 		const bool fl_fast = lf_on && W == 16u * C && ((yal | sy) & 15u) == 0 && ((ual | suv | vofs) & 7u) == 0;
-#endif
 		{
 			const int hh = lane0 >> 5, ln = lane0 & 31;
 			const uint32_t rr = rA + (uint32_t)hh;
@@ -1226,7 +1061,6 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 			fl_bits = (row_ok && ln < 20 && prowY < H ? 1u : 0u) | (ln >= 16 && nlast ? 2u : 0u) |
 			          (((yal + fl_offY) & 15u) == 0 ? 4u : 0u) | (row_ok && ln < 24 && prowC < CH ? 8u : 0u) |
 			          (kc >= 8 && nlast ? 16u : 0u) | (((ual + fl_offC) & 7u) == 0 ? 32u : 0u);
-#if VP8G_FAST_FLUSH
 			// Whole-piece frames (fl_fast): every row piece of a column inside the frame is a full,
 			// aligned 16-B / 8-B store.  The offsets then fold the lane's column shift (the left MB for
 			// tile rows >= 4) in, and a lane that never stores to HBM this pair (outside the crop, or
@@ -1252,7 +1086,6 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 				fl_offC = (fl_bits & 8u) && !(fl_bits & 16u) ? fl_offC - shc * 8u : kNoStore;
 				fl_bits = (fl_bits & 3u) == 3u ? lcY : ((fl_bits & 24u) == 24u ? (lcC | 0x40000000u) : ~0u);  // (bit 2 / 16 alone: lanes 20..31)
 			}
-#endif
 		}
 		// The step's 32 bytes per lane, loaded one step ahead.  One variable carried around the loop
 		// and reloaded right after its last use (the dequantisation), so no register copy -- which
@@ -1270,21 +1103,15 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 			// lane-dependent LDS addresses out of the loop would exhaust the VGPR budget.
 			int lane = lane0;
 			asm volatile("" : "+v"(lane));
-#if VP8G_LAUNDER
 			// The same for the loop-invariant per-lane words and the frame flags: comparisons on them
 			// would otherwise be hoisted as 64-bit lane masks, which exhaust the SGPRs and are spilled
 			// to VGPR lanes (a v_readlane pair, plus a hazard wait, per use per step).
 			asm volatile("" : "+v"(bt_l), "+v"(fl_bits), "+s"(flags_l));
-#if VP8G_FAST_FLUSH
 			asm volatile("" : "+v"(fl_srcY), "+v"(fl_srcC));
-#endif
-#if VP8G_FAST_LF
 			asm volatile("" : "+v"(lf_vp), "+v"(lf_hp));
-#endif
 			const bool lf_on = (flags_l & VP8G_F_LOOPFILTER) != 0;
 			const bool simple = (flags_l & VP8G_F_SIMPLE) != 0;
 			const bool lf_only = (flags_l & VP8G_F_LF_ONLY) != 0;
-#endif
 			const int hh = lane >> 5, ln = lane & 31;
 			const uint32_t r = rA + (uint32_t)hh;
 			const int c = (int)t - 2 * hh;
@@ -1298,13 +1125,10 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 			[[maybe_unused]] uint8_t* const abUV = hv + kAbUV;  // (the predictor role word carries it)
 			uint8_t* const left = hv + kLeft;
 
-			// per-half side info (lanes 26..29 / 58..61 hold it)
 			// per-half side info, held by lanes 26..29 / 58..61: fetched with ds_bpermute (LDS
 			// crossbar, no LDS memory) instead of readlane + per-half select
-#if VP8G_DQ_B128
 			// (the four segments' dequant factors of this lane's class, read before the side info is known)
 			const u32x4 dq4 = *(const u32x4*)(smem + kDqTable + tabo + 16 * (ln < 16 ? 0 : (ln < 24 ? 1 : 2)));
-#endif
 			const int sdl = (hh ? 58 : 26) * 4;
 			const int ymode = __builtin_amdgcn_ds_bpermute(sdl, (int)cur.side);
 			const int uvmode = __builtin_amdgcn_ds_bpermute(sdl + 4, (int)cur.side);
@@ -1333,7 +1157,6 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 				// Packed int16 pairs: w[2r + h] = row r, columns 2h, 2h+1.  Dequantisation and the
 				// vertical pass wrap mod 2^16 exactly like the reference's int16 stores; the
 				// horizontal pass (whose (x + 4) >> 3 needs the full-precision sum) runs in 32 bits.
-#if VP8G_DQ_B128
 				uint32_t fdcac;  // (dc, ac) int16 pair: dq4[seg] by two v_cndmask levels
 				{
 					const uint64_t m1 = __builtin_amdgcn_ballot_w64((seg & 1) != 0), m2 = __builtin_amdgcn_ballot_w64((seg & 2) != 0);
@@ -1342,11 +1165,6 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 					asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(hi) : "v"(dq4.z), "v"(dq4.w), "s"(m1));
 					asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(fdcac) : "v"(lo), "v"(hi), "s"(m2));
 				}
-#else
-				const int cls = ln < 16 ? 0 : (ln < 24 ? 1 : 2);  // Y1, UV, Y2 factors
-				const uint32_t* dqt = (const uint32_t*)(smem + kDqTable + tabo) + seg * 3 + cls;
-				const uint32_t fdcac = *dqt;  // (dc, ac) int16 pair
-#endif
 				const uint32_t facac = __builtin_amdgcn_perm(fdcac, fdcac, 0x03020302u);
 				uint32_t w[8] = {pk_mul(cur.a.x, fdcac), pk_mul(cur.a.y, facac), pk_mul(cur.a.z, facac), pk_mul(cur.a.w, facac),
 				                 pk_mul(cur.b.x, facac), pk_mul(cur.b.y, facac), pk_mul(cur.b.z, facac), pk_mul(cur.b.w, facac)};
@@ -1358,27 +1176,6 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 				if (__ballot(act && !bpred) != 0ull) {
 					PRIO(10);
 					const bool wl = ln >= 26 && ln < 30;
-#if VP8G_WHT_LOCAL
-					// every WHT lane holds the whole Y2 block: it runs the vertical pass of both column pairs
-					// itself and keeps its own row (ln - 26) -- no LDS round trip between the passes
-					if (wl) {
-						uint32_t v[8];
-#pragma unroll
-						for (int h = 0; h < 2; h++) {
-							const uint32_t a1 = pk_add(w[h], w[6 + h]), b1 = pk_add(w[2 + h], w[4 + h]);
-							const uint32_t c1 = pk_sub(w[2 + h], w[4 + h]), d1 = pk_sub(w[h], w[6 + h]);
-							v[h] = pk_add(a1, b1), v[2 + h] = pk_add(c1, d1), v[4 + h] = pk_sub(a1, b1), v[6 + h] = pk_sub(d1, c1);
-						}
-						const bool r1 = ((ln - 26) & 1) != 0, r2 = ((ln - 26) & 2) != 0;
-						const uint32_t tx = r2 ? (r1 ? v[6] : v[4]) : (r1 ? v[2] : v[0]);
-						const uint32_t ty = r2 ? (r1 ? v[7] : v[5]) : (r1 ? v[3] : v[1]);
-						uint8_t* const q = hv + kWht + 8 * (ln - 26);
-						const int q0 = lo_s16(tx), q1 = hi_s16(tx), q2 = lo_s16(ty), q3 = hi_s16(ty);
-						const int a1 = q0 + q3 + 3, b1 = q1 + q2, c1 = q1 - q2, d1 = q0 - q3 + 3;
-						st64(q, u32x2{pack2((a1 + b1) >> 3, (c1 + d1) >> 3), pack2((a1 - b1) >> 3, (d1 - c1) >> 3)});
-					}
-					if (false) {
-#endif
 					{
 						const int h = ln & 1;
 						const uint32_t r0 = h ? w[1] : w[0], r1 = h ? w[3] : w[2], r2 = h ? w[5] : w[4], r3 = h ? w[7] : w[6];
@@ -1399,21 +1196,17 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 						const int a1 = q0 + q3 + 3, b1 = q1 + q2, c1 = q1 - q2, d1 = q0 - q3 + 3;
 						st64(q, u32x2{pack2((a1 + b1) >> 3, (c1 + d1) >> 3), pack2((a1 - b1) >> 3, (d1 - c1) >> 3)});
 					}
-#if VP8G_WHT_LOCAL
-					}
-#endif
 					wave_lds_sync();
 					if (ln < 16 && !bpred) w[0] = (w[0] & 0xFFFF0000u) | *(const uint16_t*)(hv + kWht + 2 * ln);
 					PRIO(0);
 				}
-				auto wht_dc = [&]() -> uint32_t { return 0u; };  // (round 4 measured adding the WHT's DC late, +0.5 %: DESIGN §6)
 				// inverse DCT (RFC 14.4), the whole block per lane.  DC-only shortcut when no lane of the wave
 				// has an AC coefficient ((dc+4)>>3 everywhere, exact); a column-pair-0 transform when no
 				// block of the wave has coefficients in columns 2-3.  (Round 3 compacted the AC blocks two
 				// lanes per block through LDS: +1.6 %, removed)
 				const uint64_t mac = __ballot(anyac && ln < 24 && act);
-				auto dc_fill = [&](uint32_t dcadd) {
-					const int d = (lo_s16(pk_add(w[0], dcadd)) + 4) >> 3;
+				auto dc_fill = [&]() {
+					const int d = (lo_s16(w[0]) + 4) >> 3;
 #pragma unroll
 					for (int i = 0; i < 8; i++) rs[i] = pack2(d, d);
 				};
@@ -1426,8 +1219,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 					o[2] = pk_sub(b1, c1);
 				};
 				if (mac == 0ull) {
-					dc_fill(wht_dc());
-#if VP8G_IDCT_C01
+					dc_fill();
 				} else if (__ballot(act && ln < 24 && (w[1] | w[3] | w[5] | w[7]) != 0u) == 0ull) {
 					// Columns 2 and 3 of every block of the wave are zero (the vertical pass leaves them
 					// zero): the vertical pass of column pair 0 only, and the horizontal pass with
@@ -1437,21 +1229,15 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 					int c1[4], d1[4];
 #pragma unroll
 					for (int r = 0; r < 4; r++) {
-#if VP8G_IDCT_MH
-						c1[r] = mul_s_hi(oh[r]), d1[r] = mul_c_hi(oh[r]);
-#else
 						const int x1 = hi_s16(oh[r]);
 						c1[r] = mul_s(x1), d1[r] = mul_c(x1);
-#endif
 					}
-					const uint32_t dcadd = wht_dc();
 #pragma unroll
 					for (int r = 0; r < 4; r++) {
-						const int x0 = lo_s16(pk_add(oh[r], dcadd)) + 4;
+						const int x0 = lo_s16(oh[r]) + 4;
 						rs[2 * r] = pack2((x0 + d1[r]) >> 3, (x0 + c1[r]) >> 3);
 						rs[2 * r + 1] = pack2((x0 - c1[r]) >> 3, (x0 - d1[r]) >> 3);
 					}
-#endif
 				} else {
 					uint32_t o[8];
 #pragma unroll
@@ -1461,22 +1247,16 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 #pragma unroll
 						for (int r = 0; r < 4; r++) o[2 * r + h] = oh[r];
 					}
-					// horizontal pass: the multiplications first (columns 1, 3), then the sums with column 0
-					// (which carries the late DC) and column 2
+					// horizontal pass: the multiplications first (columns 1, 3), then the sums with columns 0, 2
 					int c1[4], d1[4];
 #pragma unroll
 					for (int r = 0; r < 4; r++) {
-#if VP8G_IDCT_MH
-						c1[r] = mul_s_hi(o[2 * r]) - mul_c_hi(o[2 * r + 1]), d1[r] = mul_c_hi(o[2 * r]) + mul_s_hi(o[2 * r + 1]);
-#else
 						const int x1 = hi_s16(o[2 * r]), x3 = hi_s16(o[2 * r + 1]);
 						c1[r] = mul_s(x1) - mul_c(x3), d1[r] = mul_c(x1) + mul_s(x3);
-#endif
 					}
-					const uint32_t dcadd = wht_dc();
 #pragma unroll
 					for (int r = 0; r < 4; r++) {
-						const int x0 = lo_s16(pk_add(o[2 * r], dcadd)), x2 = lo_s16(o[2 * r + 1]);
+						const int x0 = lo_s16(o[2 * r]), x2 = lo_s16(o[2 * r + 1]);
 						const int a1 = x0 + x2 + 4, b1 = x0 - x2 + 4;
 						rs[2 * r] = pack2((a1 + d1[r]) >> 3, (b1 + c1[r]) >> 3);
 						rs[2 * r + 1] = pack2((b1 - c1[r]) >> 3, (a1 - d1[r]) >> 3);
@@ -1500,7 +1280,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 				const uint32_t lag = xin ? 5u : 4u;
 				const uint32_t ahead = (t + lag < CP2) ? t + lag : CP2;
 				if (xin) wait_prog(0u, (k - 1) * CP2 + ahead, true);
-				else wait_prog((uint32_t)((wave + NW - dg) % NW), ((g - dg) << kProgShift) + ahead, false, VP8G_SPLIT_PROG ? progm : prog);
+				else wait_prog((uint32_t)((wave + NW - dg) % NW), ((g - dg) << kProgShift) + ahead, false);
 			}
 			if (kS && xin) {
 				// mailbox -> this part's LDS ctx: rec[t + 1] and lf[t] now (loaded last step; at t = 0
@@ -1530,9 +1310,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 
 			// ---------------------------------------------- borders + loop-filter top strip
 			PRIO(2);
-#if VP8G_PRED_ROLE
 			const u32x2 prole = ld64(smem + kRoleTab + 8 * ln);  // (used by the predictor; rides the border loads' round trip)
-#endif
 			if (act) {
 				const bool top = r == 0;
 				if (lf_only) {
@@ -1567,8 +1345,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 					const uint32_t v = kind == 0 ? vabove : (kind == 1 ? 0x81818181u : vcorner);
 					if (ln < 20 && (kind != 1 || c == 0)) st32(hv + (bt & 0xFFFu), v);
 				}
-				if (!(VP8G_SPLIT_PROG && !xin) && lf_on && !top && ln >= 20) {  // filter state of the MB above (both modes; roles in kBorderTab)
-#if VP8G_FAST_STRIP
+				if (lf_on && !top && ln >= 20) {  // filter state of the MB above (both modes; roles in kBorderTab)
 					const uint32_t bt = bt_l;
 					const bool ly = (bt >> 22) & 1u;
 					const uint32_t lo = rec_off(cu) + ((bt >> 12) & 0xFFu);
@@ -1577,14 +1354,6 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 					const u32x2 s0 = ctx.rd64(lo), s1 = ctx.rd64(lo + 8);
 					if (ly) st64(td, s0), st64(td + 8, s1);
 					else stc64(td, s0);
-#else
-					const bool ly = ln < 24;
-					const int p = (ln - 24) >> 2, tr = ly ? ln - 20 : (ln - 24) & 3;
-					const uint32_t lo = lf_off(cu) + (ly ? tr * 16 : 64 + p * 32 + tr * 8);
-					uint8_t* const td = ly ? tY + tr * kTP + slot * 16 : tC + p * kCV + tr * kTP + slot * 8;
-					if (ly) st64(td, ctx.rd64(lo)), st64(td + 8, ctx.rd64(lo + 8));
-					else stc64(td, ctx.rd64(lo));
-#endif
 				}
 			}
 			wave_lds_sync();
@@ -1597,27 +1366,13 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 					// whole-block predictors (RFC 12.2; reference vp8_recon.c:152-212, 533-560, 605-651),
 					// one 4x4 block per lane, branch-free: every mode is sat8(L' + A' + K) with
 					// L' = L & mL, A' = A & mA (DC: K = dc value; V: mA; H: mL; TM: both, K = -P)
-#if VP8G_PRED_ROLE
 					const bool yl = (prole.x >> 22) & 1u;
 					const uint8_t* ab = hv + (prole.x & 0x7FFu);
 					const uint8_t* lc = hv + (prole.y & 0x7FFu);
-#else
-					const bool yl = ln < 16;
-					const int p = (ln - 16) >> 2;  // chroma plane (chroma lanes)
-					const int blk = yl ? ln : (ln & 3);
-					const int bx = yl ? (blk & 3) : (blk & 1), by = yl ? (blk >> 2) : (blk >> 1);
-					const uint8_t* ab = yl ? abY + 16 : abUV + 16 * p + 8;
-					const uint8_t* lc = yl ? left : left + 16 + 8 * p;
-#endif
 					const int mode = yl ? (ymode > 4 ? 0 : ymode) : (uvmode > 3 ? 0 : uvmode);
 					const u32x2 a01 = ld64(ab), a23 = ld64(ab + 8), l01 = ld64(lc), l23 = ld64(lc + 8);
-#if VP8G_PRED_ROLE
 					const uint32_t aw = ld32(hv + __builtin_amdgcn_ubfe(prole.x, 11u, 11u));
 					const uint32_t lw = ld32(lc + 4u * __builtin_amdgcn_ubfe(prole.y, 22u, 2u));
-#else
-					const uint32_t aw = ld32(ab + 4 * bx);
-					const uint32_t lw = ld32(lc + 4 * by);
-#endif
 					const int P = (int)ab[-1];
 					const uint32_t sa2 = __builtin_amdgcn_sad_u8(a01.y, 0u, __builtin_amdgcn_sad_u8(a01.x, 0u, 0u));
 					const uint32_t sl2 = __builtin_amdgcn_sad_u8(l01.y, 0u, __builtin_amdgcn_sad_u8(l01.x, 0u, 0u));
@@ -1626,35 +1381,23 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 					const bool ha = r > 0, hl = c > 0;
 					const uint32_t sum = (ha ? (yl ? sa4 : sa2) : 0u) + (hl ? (yl ? sl4 : sl2) : 0u);
 					const int shift = (yl ? 3 : 2) + (ha ? 1 : 0) + (hl ? 1 : 0);  // 16 or 8 samples per edge
-#if VP8G_PRED_FLAT
 					// (no branch around the sums: every load of the predictor issued in one LDS round trip)
 					int dcv;
 					asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(dcv) : "v"(128), "v"((int)((sum + (1u << (shift - 1))) >> shift)),
 					    "s"(__builtin_amdgcn_ballot_w64(ha || hl)));
-#else
-					const int dcv = (ha || hl) ? (int)((sum + (1u << (shift - 1))) >> shift) : 128;
-#endif
 					// two pixels per op as int16 pairs (|residual| < 2^14, so nothing wraps)
 					const uint32_t mA = (mode == 1 || mode == 3) ? 0x00FF00FFu : 0u;
 					const uint32_t mL = (mode == 2 || mode == 3) ? 0x00FF00FFu : 0u;
 					const int K = (mode == 3 ? -P : 0) + (mode == 0 ? dcv : 0);
 					const uint32_t K2 = __builtin_amdgcn_perm((uint32_t)K, (uint32_t)K, 0x05040100u);  // K in both halves
-#if VP8G_PRED_ROLE
 					uint8_t* dst = hv + __builtin_amdgcn_ubfe(prole.y, 11u, 11u) + (slot ? (yl ? 16u : 8u) : 0u);
-#else
-					uint8_t* dst = yl ? tY + (4 + 4 * by) * kTP + slot * 16 + 4 * bx
-					                  : tC + p * kCV + (4 + 4 * by) * kTP + slot * 8 + 4 * bx;
-#endif
 					const uint32_t* const rw = rs;  // this lane's own block
 					const uint32_t A01 = pk_add(__builtin_amdgcn_perm(aw, aw, 0x0C010C00u) & mA, K2);
 					const uint32_t A23 = pk_add(__builtin_amdgcn_perm(aw, aw, 0x0C030C02u) & mA, K2);
 					uint32_t wv[4];
 					// only TM_PRED's predictor can leave [0, 255]: its clamp runs when some lane uses it
-					// (VP8G_SATPK: the final clamp + byte packing by two v_sat_pk_u8_i16 and one shift-or)
-					auto pack_row = [&](uint32_t q01, uint32_t q23) -> uint32_t {
-						if constexpr (VP8G_SATPK) return sat_pk(q01) | (sat_pk(q23) << 16);
-						else return __builtin_amdgcn_perm(pk_clamp255(q23), pk_clamp255(q01), 0x06040200u);
-					};
+					// (the final clamp + byte packing by two v_sat_pk_u8_i16 and one shift-or)
+					auto pack_row = [&](uint32_t q01, uint32_t q23) -> uint32_t { return sat_pk(q01) | (sat_pk(q23) << 16); };
 					if (__ballot(mode == 3) != 0ull) {
 #pragma unroll
 						for (int rr = 0; rr < 4; rr++) {
@@ -1672,22 +1415,12 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 					for (int rr = 0; rr < 4; rr++) st32(dst + rr * kTP, wv[rr]);
 					// the MB's unfiltered bottom row -> ctx_rec[c] (the next MB row's above row) and its
 					// right column -> the left column of the next MB (reference vp8_recon.c:395-421)
-#if VP8G_PRED_ROLE
 					if ((prole.x >> 23) & 1u) ctx.wr32(rec_off(cu) + (prole.x >> 25), wv[3]);
 					if ((prole.x >> 24) & 1u) {
 						const uint32_t c01 = __builtin_amdgcn_perm(wv[1], wv[0], 0x0C0C0703u);
 						const uint32_t c23 = __builtin_amdgcn_perm(wv[3], wv[2], 0x0C0C0703u);
 						st32(const_cast<uint8_t*>(lc) + 4u * __builtin_amdgcn_ubfe(prole.y, 22u, 2u), __builtin_amdgcn_perm(c23, c01, 0x05040100u));
 					}
-#else
-					const int last = yl ? 3 : 1;
-					if (by == last) ctx.wr32(rec_off(cu) + (yl ? 4 * bx : 16 + 8 * p + 4 * bx), wv[3]);
-					if (bx == last) {
-						const uint32_t c01 = __builtin_amdgcn_perm(wv[1], wv[0], 0x0C0C0703u);
-						const uint32_t c23 = __builtin_amdgcn_perm(wv[3], wv[2], 0x0C0C0703u);
-						st32((yl ? left : left + 16 + 8 * p) + 4 * by, __builtin_amdgcn_perm(c23, c01, 0x05040100u));
-					}
-#endif
 				}
 				wave_lds_sync();
 				SUBMARK(20);
@@ -1711,17 +1444,15 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 					const int16_t* const rsp = (const int16_t*)(hv + kResid) + p + 32 * g;    // + 16 b0
 					const u32x4* const tabp = (const u32x4*)(smem + kBpTable) + p * (kBpEntry / 16);  // + 16 mode entries
 					const bool col3 = cc == 3;
-#if VP8G_BP_REGION
 					// (one exec region for the whole wavefront: group 0 has a sub-block at every step and
 					// group 1 at steps 2..7, so only steps 0, 1, 8, 9 narrow the lanes again)
 					if (bp_lane) {
-#endif
 #pragma unroll
 					for (int s = 0; s < 10; s++) {
 						const int i0 = s <= 3 ? 0 : (s - 2) >> 1;
 						const int j0 = s - 2 * i0;  // g = 0: (i0, j0); g = 1: (i0 + 1, j0 - 2)
 						const bool v0 = j0 <= 3, v1 = i0 + 1 <= 3 && j0 >= 2;
-						const bool valid = (VP8G_BP_REGION || bp_lane) && (g ? v1 : v0);
+						const bool valid = g ? v1 : v0;
 						if (valid) {
 							const int b0 = 4 * i0 + j0;
 							const int mb0 = v0 ? (int)((bmw[b0 >> 2] >> (8 * (b0 & 3))) & 0xFFu) : 0;
@@ -1741,19 +1472,11 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 							const uint32_t lo = __builtin_amdgcn_perm(ey, lw, tb.x);
 							const uint32_t hi = __builtin_amdgcn_perm(a47, a03, tb.x);
 							const uint32_t x3 = (hi & tb.y) | (lo & ~tb.y);  // bytes 0..2 = x, y, z
-#if VP8G_BP_DCFOLD
-							// every mode in one signed dot product over the byte-biased edge, DC_PRED's above row
-							// added by v_sad_u8 under the entry's mask
-							const u32x4 tb2 = tabp[16 * (kBpEntry / 16) * mode + 1];
-							const int dot = __builtin_amdgcn_sdot4((int)(x3 ^ 0x80808080u), (int)tb.z, (int)tb.w, false);
-							const int pred = sat8((int)__builtin_amdgcn_sad_u8(a03 & tb2.y, 0u, (uint32_t)dot) >> tb2.x);
-#else
 							// directional modes and TM in one signed dot product over the byte-biased edge
 							const int vdir = sat8(__builtin_amdgcn_sdot4((int)(x3 ^ 0x00808080u), (int)tb.z, (int)tb.w, false) >>
 							                      (tb.y >> 24));
 							const int vdc = (int)((__builtin_amdgcn_sad_u8(a03, 0u, __builtin_amdgcn_sad_u8(lw, 0u, 4u))) >> 3);
 							const int pred = mode == 0 ? vdc : vdir;
-#endif
 							const int px = sat8(pred + rv);
 							tpix[kBS * i0 + 4 * s] = (uint8_t)px;
 							// right pixel column of a sub-block: left column of the next sub-block column (in
@@ -1764,9 +1487,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 						}
 						wave_lds_sync();
 					}
-#if VP8G_BP_REGION
 					}
-#endif
 				}
 			}
 			wave_lds_sync();
@@ -1776,31 +1497,6 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 			// corner for the next MB is taken at its border setup)
 			STAMP(4);
 
-#if VP8G_SPLIT_PROG
-			// prediction context of this step is complete: successors may start their borders
-			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-			if (lane == 0 && wave != VP8G_TEST_STALL_WAVE)
-				__hip_atomic_store(progm + wave, (g << kProgShift) + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-			if (!xin) {
-				// the filter state of the MB above (ctx_lf) is written by the predecessor's flush: wait for
-				// its full step, then copy it into the tile's top rows (roles in kBorderTab)
-				PRIO(1);
-				if (has_pred && !dead && !(VP8G_ABLATE & 8)) {
-					const uint32_t ahead = (t + 4u < CP2) ? t + 4u : CP2;
-					wait_prog((uint32_t)((wave + NW - dg) % NW), ((g - dg) << kProgShift) + ahead, false, prog);
-				}
-				if (act && lf_on && r > 0 && ln >= 20) {
-					const uint32_t bt = bt_l;
-					const bool ly = (bt >> 22) & 1u;
-					const uint32_t lo = rec_off(cu) + ((bt >> 12) & 0xFFu);
-					uint8_t* const td = hv + (bt & 0xFFFu) + (slot ? (ly ? 16u : 8u) : 0u);
-					const u32x2 s0 = ctx.rd64(lo), s1 = ctx.rd64(lo + 8);
-					if (ly) st64(td, s0), st64(td + 8, s1);
-					else stc64(td, s0);
-				}
-				wave_lds_sync();
-			}
-#endif
 			// ---------------------------------------------- loop filter MB(r, c)
 			PRIO(5);
 			if (lf_on && !(VP8G_ABLATE & 1)) {
@@ -1809,7 +1505,6 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 				const bool en = act && E != 0;
 				if (__ballot(en) != 0ull) {
 					const bool inner = hasc != 0 || bpred;
-#if VP8G_FAST_LF
 					// (per-pair lane words: tile offsets at slot 0 | slot 1 << 16, from the wave's area)
 					LfLine L;
 					{
@@ -1818,15 +1513,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 						L.Mp = wv + __builtin_amdgcn_ubfe(lf_vp, sl16, 16u);
 						L.Lp = L.Mp + (slot ? -4 : (ln < 16 ? 28 : 12));
 						L.colp = wv + __builtin_amdgcn_ubfe(lf_hp, sl16, 16u);
-						// (VP8G_LF_REDIRECT) chroma lanes' bytes 10..17 land in the half's B_PRED residual area,
-						// free after B_PRED: 16 distinct dword-spaced bases per half
-						uint8_t* const scr = hv + kResid + 4 * (ln & 15);
-						L.Mhi = ln < 16 ? L.Mp : scr - 6;
-						L.colhi = ln < 16 ? L.colp : scr - 10 * kTP;
 					}
-#else
-					const LfLine L = lf_lines(tY, tC, ln, slot);
-#endif
 					if (simple) lf_mb<true>(L, ln, en, c > 0, r > 0, inner, E, I, Tt);
 					else lf_mb<false>(L, ln, en, c > 0, r > 0, inner, E, I, Tt);
 				}
@@ -1899,7 +1586,6 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 					poffC = off, pcntC = vis && !full ? min(CW - colpx, 8u) : 0u;
 				}
 			}
-#if VP8G_FAST_FLUSH
 			else if (fl_fast) {
 				// whole-piece frame: the folded per-pair offsets and tile sources (see fl_fast); the rows
 				// the next MB row still filters go to ctx_lf instead (fl_bits = their ctx_lf offset)
@@ -1928,7 +1614,6 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) VP8G_KATTR void 
 				}
 #endif
 			}
-#endif
 			else {
 				{  // luma: ln 0..3 the MB above's bottom rows (this column, final now); 4..19 the left MB
 					const bool top = ln < 4;
@@ -2120,13 +1805,7 @@ int device_cus() {
 }
 
 uint32_t pick_waves(uint32_t waves_hint, uint32_t max_mb_rows, uint32_t n_frames) {
-#ifdef VP8G_NW10  // diagnostic: 10 waves per frame at 5 waves per SIMD (needs the global context)
-	static const uint32_t kSupported[] = {1, 2, 4, 8, 10, 12, 16};
-#elif defined(VP8G_NW67)  // experiment: 6 / 7 waves per frame (fewer idle waves in a frame's last round)
-	static const uint32_t kSupported[] = {1, 2, 4, 6, 7, 8, 12, 16};
-#else
 	static const uint32_t kSupported[] = {1, 2, 4, 8, 12, 16};
-#endif
 	// default: 8 waves (two frames per CU) when the batch fills the chip; a batch with at most
 	// one frame per CU gets 16 waves per frame instead (twice the MB row pairs in flight)
 	const int n_cus = device_cus();
@@ -2263,13 +1942,6 @@ hipError_t launch_frames(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const 
 		VP8G_CASE(4)
 		VP8G_CASE(8)
 		VP8G_CASE(12)
-#ifdef VP8G_NW10
-		VP8G_CASE(10)
-#endif
-#ifdef VP8G_NW67
-		VP8G_CASE(6)
-		VP8G_CASE(7)
-#endif
 		default:
 		VP8G_CASE(16)
 	}
