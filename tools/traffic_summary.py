@@ -34,6 +34,36 @@ for line in open(src / "trace_bench.log"):
 if bench_line:
     (prof / f"{tag}_trace_bench.json").write_text(json.dumps(bench_line, indent=1) + "\n")
 
+# Same process, same box (verdict r04 #2): the per-dispatch durations of the bench kernel from the
+# kernel trace of the very bench run whose line is above.  The timed steps are the bench's last
+# dispatches of frame_kernel before its parity launch; the median over every dispatch but the first
+# (cold) one is what the line's kernel time is compared with, and frac is recomputed from it.
+traces = glob.glob(str(src / "trace" / "**" / "*kernel_trace.csv"), recursive=True)
+if traces and bench_line:
+    durs = []
+    for r in csv.DictReader(open(traces[0])):
+        if "frame_kernel" in r["Kernel_Name"]:
+            durs.append((int(r["Start_Timestamp"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6))
+    durs = [d for _, d in sorted(durs)]
+    warm = durs[1:]
+    med = sorted(warm)[len(warm) // 2]
+    alg = bench_line["roofline"]["algorithmic_bytes_per_launch"]
+    same = {
+        "tag": tag,
+        "source": "rocprofv3 --kernel-trace of the bench run whose line is in " + f"{tag}_trace_bench.json" +
+                  " (same process, same box); frame_kernel dispatches in launch order",
+        "dispatch_ms": [round(d, 3) for d in durs],
+        "median_ms_excluding_first": round(med, 3),
+        "bench_ms_per_step": bench_line["ms_per_step"],
+        "bench_kernel_ms_per_step": bench_line.get("kernel_ms_per_step"),
+        "kernel_le_step": med <= bench_line["ms_per_step"],
+        "frac_from_trace": round(alg / (med * 1e-3) / 1e9 / bench_line["roofline"]["peak"], 4),
+        "frac_bench_line": bench_line["roofline"]["frac"],
+    }
+    same["frac_rel_diff"] = round(abs(same["frac_from_trace"] - same["frac_bench_line"]) / same["frac_bench_line"], 4)
+    (prof / f"{tag}_trace_vs_line.json").write_text(json.dumps(same, indent=1) + "\n")
+    print(json.dumps({k: v for k, v in same.items() if k != "dispatch_ms"}, indent=1))
+
 
 def per_dispatch(counter):
     f = glob.glob(str(src / f"pmc_{counter}" / "**" / "*counter_collection.csv"), recursive=True)[0]

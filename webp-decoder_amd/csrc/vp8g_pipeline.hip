@@ -408,15 +408,22 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 	}
 	uint64_t chunk_mbs_tok = kTokChunkMbs, chunk_mbs_pk = kChunkMbs;
 	{
-		// four chunk slots (two per chunk kind) of ~1.3 KB per MB each (+ payloads): keep all of
-		// them within ~3/8 of the free device memory, so a device shared with other work gets
-		// smaller chunks instead of a failed allocation (EIO for every frame)
+		// four chunk slots (two per chunk kind): host-m05 chunks ~1.5 KB per MB, device-m05 chunks
+		// ~1.3 KB per MB (+ payloads).  All four stay within ~3/8 of the free device memory, so a
+		// device shared with other work gets smaller chunks instead of a failed allocation (EIO for
+		// every frame); the device-m05 slots get what the (small) host-m05 slots leave.  (Round 5:
+		// the old cap, free / 16384 MBs for every slot, cut 768 device frames into two m05 launches
+		// on a 288-GB card; the second one then waited behind the first whenever their streams
+		// shared a hardware queue -- DESIGN.md §12.)
 		size_t fr = 0, tot = 0;
 		if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr) {
-			const uint64_t cap = (uint64_t)fr / 16384u;  // = fr * 3/8 / (4 slots x 1.5 KB)
-			const uint64_t floor_mbs = 1u << 15;         // one 4K frame and change
-			if (cap < chunk_mbs_tok) chunk_mbs_tok = cap > floor_mbs ? cap : floor_mbs;
-			if (cap < chunk_mbs_pk) chunk_mbs_pk = cap > floor_mbs ? cap : floor_mbs;
+			const uint64_t budget = (uint64_t)fr / 8u * 3u;
+			const uint64_t floor_mbs = 1u << 15;  // one 4K frame and change
+			const uint64_t cap_pk = budget / (4u * 1536u);
+			if (cap_pk < chunk_mbs_pk) chunk_mbs_pk = cap_pk > floor_mbs ? cap_pk : floor_mbs;
+			const uint64_t pk_bytes = 2u * chunk_mbs_pk * 1536u;
+			const uint64_t cap_tok = budget > pk_bytes ? (budget - pk_bytes) / (2u * 1331u) : 0u;
+			if (cap_tok < chunk_mbs_tok) chunk_mbs_tok = cap_tok > floor_mbs ? cap_tok : floor_mbs;
 		}
 	}
 	for (uint32_t i = 0; i < n; i++) memset(&outs[i], 0, sizeof(outs[i]));
@@ -511,7 +518,18 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 		}                            \
 	} while (0)
 
-	for (hipStream_t& st : streams) PTRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "stream");
+	// The device-m05 slots' streams (0, 1) at the lowest stream priority, the others at the default:
+	// HIP keeps a pool of hardware queues per priority, so a host-m05 chunk never sits in one hardware
+	// queue behind a device-m05 kernel (~0.5-1.5 s, one frame's serial bool decoding) -- streams
+	// beyond GPU_MAX_HW_QUEUES share queues, and work on a shared queue runs in order.
+	{
+		int least = 0, greatest = 0;
+		if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = 0;
+		for (int i = 0; i < 4; i++)
+			PTRY(i < 2 ? hipStreamCreateWithPriority(&streams[i], hipStreamNonBlocking, least)
+			           : hipStreamCreateWithFlags(&streams[i], hipStreamNonBlocking),
+			     "stream");
+	}
 	for (Copier& c : copiers) {
 		PTRY(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking), "stream");
 		c.th = std::thread([&c] { c.run(); });
