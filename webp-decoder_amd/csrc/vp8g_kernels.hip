@@ -50,6 +50,13 @@
 #endif
 constexpr int kPrioTab[11] = {VP8G_PRIO_TABLE, VP8G_PRIO_LF, VP8G_PRIO_WHT};
 #define PRIO(ph) __builtin_amdgcn_s_setprio(kPrioTab[ph])
+// PRIO_AFTER(ph, prev...): PRIO(ph), elided when it would not change the level set by any of the
+// phases that can come right before it (7 of the 15 s_setprio per step with the default table)
+template <int ph, int... prev>
+__device__ __forceinline__ void prio_after() {
+	if constexpr (((kPrioTab[ph] != kPrioTab[prev]) || ...)) __builtin_amdgcn_s_setprio(kPrioTab[ph]);
+}
+#define PRIO_AFTER(ph, ...) prio_after<ph, __VA_ARGS__>()
 #ifndef VP8G_ABLATE
 #define VP8G_ABLATE 0
 #endif
@@ -536,9 +543,9 @@ DEV void lf_mb(const LfLine& L, int ln, bool en, bool mb_v, bool mb_h, bool inne
 		// ds_write_b8 -- merged wide accesses cost vector instructions to (un)pack)
 		uint8_t* const Lp = L.Lp;
 		uint8_t* const Mp = L.Mp;
-		PRIO(8);
+		PRIO_AFTER(8, 5);
 		gather20<1, 1>(Lp, Mp, px);
-		PRIO(9);
+		PRIO_AFTER(9, 8);
 		lf_line<kSimple>(px, en && mb_v, en && inner, isy, E, I, T);
 		// the row written back as dwords -- bytes the filter leaves alone are rewritten unchanged;
 		// 3 / 5 LDS stores instead of 9 / 17 byte stores, for ~15 packing instructions
@@ -556,9 +563,9 @@ DEV void lf_mb(const LfLine& L, int ln, bool en, bool mb_v, bool mb_h, bool inne
 	// horizontal edges: one line per lane down a pixel column (tile rows 0..19, pitch kTP)
 	{
 		uint8_t* const colp = L.colp;
-		PRIO(8);
+		PRIO_AFTER(8, 9);
 		gather20<kTP, kTP>(colp, colp + 4 * kTP, px);
-		PRIO(9);
+		PRIO_AFTER(9, 8);
 		lf_line<kSimple>(px, en && mb_h, en && inner, isy, E, I, T);
 		if (wr) {
 #pragma unroll
@@ -821,7 +828,9 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 	uint32_t* const gp_out = kS ? gprog + f * K + part : nullptr;
 
 #ifdef VP8G_STAMPS
-	uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+	// phases 0..7 as below; sub-phases (round 5): 10 side info, 11 iWHT (within the residual),
+	// 12 whole-block prediction (within recon); 8 and 9 hold the launch clocks
+	uint64_t st_acc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 	uint64_t st_prev = __builtin_amdgcn_s_memtime();
 	if (blockIdx.x == 0 && lane0 == 0 && wave < 32) g_vp8g_wave_times[2 * wave] = __builtin_amdgcn_s_memrealtime();
 	const uint64_t st_t0 = __builtin_amdgcn_s_memrealtime();
@@ -1143,6 +1152,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			                        (uint32_t)__builtin_amdgcn_ds_bpermute(bml, (int)cur.a.z),
 			                        (uint32_t)__builtin_amdgcn_ds_bpermute(bml, (int)cur.a.w)};
 
+			STAMP(10);
 			// ---------------------------------------------- residual (no spatial dependency)
 			SUBMARK(30);
 			PRIO(0);
@@ -1200,6 +1210,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					if (ln < 16 && !bpred) w[0] = (w[0] & 0xFFFF0000u) | *(const uint16_t*)(hv + kWht + 2 * ln);
 					PRIO(0);
 				}
+				STAMP(11);
 				// inverse DCT (RFC 14.4), the whole block per lane.  DC-only shortcut when no lane of the wave
 				// has an AC coefficient ((dc+4)>>3 everywhere, exact); a column-pair-0 transform when no
 				// block of the wave has coefficients in columns 2-3.  (Round 3 compacted the AC blocks two
@@ -1262,7 +1273,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 						rs[2 * r + 1] = pack2((b1 - c1[r]) >> 3, (a1 - d1[r]) >> 3);
 					}
 				}
-				if (ln < 16) {
+				if (ln < 16 && bpred) {  // (only the B_PRED pixel lanes of a B_PRED half read it)
 					uint8_t* rp = hv + kResid + ln * 32;
 					st128(rp, u32x4{rs[0], rs[1], rs[2], rs[3]});
 					st128(rp + 16, u32x4{rs[4], rs[5], rs[6], rs[7]});
@@ -1309,7 +1320,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			STAMP(1);
 
 			// ---------------------------------------------- borders + loop-filter top strip
-			PRIO(2);
+			PRIO_AFTER(2, 1);
 			const u32x2 prole = ld64(smem + kRoleTab + 8 * ln);  // (used by the predictor; rides the border loads' round trip)
 			if (act) {
 				const bool top = r == 0;
@@ -1423,10 +1434,11 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					}
 				}
 				wave_lds_sync();
+				STAMP(12);
 				SUBMARK(20);
 				const bool bp_lane = act && bpred;
 				if (__ballot(bp_lane) != 0ull && !(VP8G_ABLATE & 2)) {
-					PRIO(4);
+					PRIO_AFTER(4, 3);
 					// B_PRED: 16 sub-blocks along the 2i+j wavefront (10 steps, <= 2 sub-blocks each;
 					// lanes 0..15 / 16..31 of a half = group g take sub-block (i0 + g, s - 2 i0 - 2 g)),
 					// one pixel per lane, from already reconstructed pixels (reference
@@ -1708,7 +1720,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 				if (lane0 == 0) __hip_atomic_store(gprog + fcur, nsplit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 			}
 			// ---------------------------------------------- publish progress
-			PRIO(7);
+			PRIO_AFTER(7, 6);
 			ctx.publish_fence();
 			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 			if (kS && xout) {
@@ -1734,7 +1746,8 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 	}
 #ifdef VP8G_STAMPS
 	if (lane0 == 0)
-		for (int i = 0; i < 8; i++) atomicAdd(&g_vp8g_stamps[i], (unsigned long long)st_acc[i]);
+		for (int i = 0; i < 14; i++)
+			if (i != 8 && i != 9) atomicAdd(&g_vp8g_stamps[i], (unsigned long long)st_acc[i]);
 	if (f == 0 && lane0 == 0 && wave < 32) g_vp8g_wave_times[2 * wave + 1] = __builtin_amdgcn_s_memrealtime();
 	if (blockIdx.x < 512 && wave < 16 && lane0 == 0) {
 		uint32_t hw, xcc;
