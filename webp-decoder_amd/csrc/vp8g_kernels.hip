@@ -62,9 +62,6 @@ __device__ __forceinline__ void prio_after() {
 #endif
 // (Rejected experiments -- their numbers are in DESIGN.md §6 -- were removed in round 5; the shipped
 // paths are unconditional now.  The remaining switches are the diagnostics above and below.)
-#ifndef VP8G_SIDE_EARLY  // (experiment) next step's side-info broadcast at the end of this step
-#define VP8G_SIDE_EARLY 0
-#endif
 // Bound of one dependency wait in s_memrealtime ticks (100 MHz): 2 s.  Test builds shorten it and
 // make one wave never publish its progress (VP8G_TEST_STALL_WAVE) to check that a stalled producer
 // ends the launch promptly with VP8G_ERR_TIMEOUT (tests/test_gpu_batch.py).
@@ -1109,12 +1106,14 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 		bst128(rY, kNoStore, u32x4{0u, 0u, 0u, 0u});
 		bst64(rC, kNoStore, u32x2{0u, 0u});
 		flags_l = (uint32_t)__builtin_amdgcn_readfirstlane((int)flags);  // (the chain's frame loop makes it a PHI)
-		// (VP8G_SIDE_EARLY) the next step's per-half side info, broadcast from the prefetched bytes at the
-		// end of the previous step (after its loop filter) instead of at the top of the step
+		// Per-half side info of a step, broadcast from the prefetched bytes of lanes 26..29 / 58..61 (and
+		// the 16 B_PRED modes from lane 25 / 57) with ds_bpermute (LDS crossbar, no LDS memory), at the
+		// top of the step.  (Round 5 fetched it at the end of the previous step, after the loop filter,
+		// to take its round trip off the step's start: +6.3 %, r05f -- the work moved in front of the
+		// publish delays the next wave, whose dependency wait is on that publish.)
 		struct Side {
 			int ymode, uvmode, seg, hasc;
 			u32x4 bmw;
-			uint32_t fdcac;  // (dc, ac) int16 pair of dequant factors of this lane's class and segment
 		};
 		// the four segments' dequant factors of a lane's class in one 16-B read, the segment's pair picked
 		// by two v_cndmask levels once the side info is known
@@ -1129,8 +1128,6 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 		};
 		auto fetch_side = [&](int lane_) -> Side {
 			const int hh_ = lane_ >> 5;
-			[[maybe_unused]] u32x4 dq4;
-			if constexpr (VP8G_SIDE_EARLY) dq4 = load_dq4(lane_ & 31);  // (issued ahead of the permutes)
 			const int sdl = (hh_ ? 58 : 26) * 4, bml = (hh_ ? 57 : 25) * 4;
 			Side sd;
 			sd.ymode = __builtin_amdgcn_ds_bpermute(sdl, (int)cur.side);
@@ -1139,12 +1136,8 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			sd.hasc = __builtin_amdgcn_ds_bpermute(sdl + 12, (int)cur.side);
 			sd.bmw = u32x4{(uint32_t)__builtin_amdgcn_ds_bpermute(bml, (int)cur.a.x), (uint32_t)__builtin_amdgcn_ds_bpermute(bml, (int)cur.a.y),
 			               (uint32_t)__builtin_amdgcn_ds_bpermute(bml, (int)cur.a.z), (uint32_t)__builtin_amdgcn_ds_bpermute(bml, (int)cur.a.w)};
-			if constexpr (VP8G_SIDE_EARLY) sd.fdcac = pick_dq(dq4, sd.seg);
-			else sd.fdcac = 0u;
 			return sd;
 		};
-		[[maybe_unused]] Side side_next;
-		if constexpr (VP8G_SIDE_EARLY) side_next = fetch_side(lane0);
 
 		for (uint32_t t = 0; t < T; t++) {
 			// Lane-derived values are recomputed every step from a laundered lane id: hoisting the
@@ -1177,10 +1170,9 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			// crossbar, no LDS memory) instead of readlane + per-half select
 			// (the four segments' dequant factors of this lane's class, read before the side info is known)
 			// (the four segments' dequant factors of this lane's class, read before the side info is known)
-			[[maybe_unused]] u32x4 dq4;
-			if constexpr (!VP8G_SIDE_EARLY) dq4 = load_dq4(ln);
+			const u32x4 dq4 = load_dq4(ln);
 			// (the half's 16 B_PRED modes come from lane 25 / 57, used by the B_PRED phase)
-			const Side side = VP8G_SIDE_EARLY ? side_next : fetch_side(lane);
+			const Side side = fetch_side(lane);
 			const int ymode = side.ymode, uvmode = side.uvmode, seg = side.seg, hasc = side.hasc;
 			const u32x4 bmw = side.bmw;
 			const bool bpred = ymode == 4;
@@ -1201,9 +1193,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 				// Packed int16 pairs: w[2r + h] = row r, columns 2h, 2h+1.  Dequantisation and the
 				// vertical pass wrap mod 2^16 exactly like the reference's int16 stores; the
 				// horizontal pass (whose (x + 4) >> 3 needs the full-precision sum) runs in 32 bits.
-				uint32_t fdcac;  // (dc, ac) int16 pair
-				if constexpr (VP8G_SIDE_EARLY) fdcac = side.fdcac;
-				else fdcac = pick_dq(dq4, seg);
+				const uint32_t fdcac = pick_dq(dq4, seg);  // (dc, ac) int16 pair
 				const uint32_t facac = __builtin_amdgcn_perm(fdcac, fdcac, 0x03020302u);
 				uint32_t w[8] = {pk_mul(cur.a.x, fdcac), pk_mul(cur.a.y, facac), pk_mul(cur.a.z, facac), pk_mul(cur.a.w, facac),
 				                 pk_mul(cur.b.x, facac), pk_mul(cur.b.y, facac), pk_mul(cur.b.z, facac), pk_mul(cur.b.w, facac)};
@@ -1559,9 +1549,6 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					else lf_mb<false>(L, ln, en, c > 0, r > 0, inner, E, I, Tt);
 				}
 			}
-			// (the side info of step t + 1 from the prefetch that has landed by now; its round trip runs
-			// under the flush instead of at the top of the next step)
-			if constexpr (VP8G_SIDE_EARLY) side_next = fetch_side(lane);
 			STAMP(5);
 
 			// ---------------------------------------------- store final pixels
