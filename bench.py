@@ -376,9 +376,9 @@ def run_workload(name, args, rank, world, dist, dev, golden, rank_factory=Rank):
     if stamps:
         acc = (C.c_ulonglong * 16)()
         lib.vp8g_debug_stamps(acc, 1)
-        slots = [10, 11, 0, 1, 2, 12, 3, 4, 5, 6, 7]  # (8, 9: the launch clocks)
+        slots = [13, 10, 11, 0, 1, 2, 12, 3, 4, 5, 6, 7]  # (8, 9: the launch clocks)
         tot = sum(acc[i] for i in slots) or 1
-        names = ["side_info", "residual_dequant_iwht", "residual_idct_park_prefetch", "dep_wait", "borders",
+        names = ["prefetch_wait", "side_info", "residual_dequant_iwht", "residual_idct_park_prefetch", "dep_wait", "borders",
                  "whole_block_prediction", "b_pred", "save_ctx", "loopfilter", "store", "publish"]
         obj["stamps"] = {k: round(acc[i] / tot, 4) for i, k in zip(slots, names)}
         obj["stamps"]["cycles_per_mb_per_wave"] = round(tot / (r.batch.total_mb * args.steps), 1)

@@ -828,8 +828,9 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 	uint32_t* const gp_out = kS ? gprog + f * K + part : nullptr;
 
 #ifdef VP8G_STAMPS
-	// phases 0..7 as below; sub-phases (round 5): 10 side info, 11 iWHT (within the residual),
-	// 12 whole-block prediction (within recon); 8 and 9 hold the launch clocks
+	// phases 0..7 as below; sub-phases (round 5): 13 the wait for the prefetched coefficients, 10 side
+	// info, 11 iWHT (within the residual), 12 whole-block prediction (within recon); 8 and 9 hold the
+	// launch clocks
 	uint64_t st_acc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 	uint64_t st_prev = __builtin_amdgcn_s_memtime();
 	if (blockIdx.x == 0 && lane0 == 0 && wave < 32) g_vp8g_wave_times[2 * wave] = __builtin_amdgcn_s_memrealtime();
@@ -1169,6 +1170,12 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			// per-half side info, held by lanes 26..29 / 58..61: fetched with ds_bpermute (LDS
 			// crossbar, no LDS memory) instead of readlane + per-half select
 			// (the four segments' dequant factors of this lane's class, read before the side info is known)
+#ifdef VP8G_STAMPS
+			// (stamps build: the wait for this step's prefetched coefficients timed on its own, sub-phase 13;
+			// vmcnt(2): all but the previous step's two output stores)
+			asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+			STAMP(13);
+#endif
 			// (the four segments' dequant factors of this lane's class, read before the side info is known)
 			const u32x4 dq4 = load_dq4(ln);
 			// (the half's 16 B_PRED modes come from lane 25 / 57, used by the B_PRED phase)
@@ -1300,6 +1307,8 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			}
 			// next step's coefficients into the same registers (the dequantisation above was cur's last
 			// use; one definition on every path, so the loop carries it without copies)
+			// (round 5: issued right after the dequantisation instead, ahead of the iWHT and iDCT: +0.6 /
+			// +1.0 %, r05h)
 			cur = prefetch(lane, cbase, sbase, csh, (int)t + 1);
 			STAMP(0);
 
@@ -1686,12 +1695,17 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					poffC = off, pcntC = vis && !full ? min(CW - colpx, 8u) : 0u;
 				}
 			}
-			bst128(rY, offY, u32x4{yl0.x, yl0.y, yl1.x, yl1.y});
-			bst64(rC, offC, cl0);
-			if (__ballot(pcntY | pcntC) != 0ull) {
-				for (uint32_t q = 0; q < pcntY; q++) outY[poffY + q] = srcY[q];
-				for (uint32_t q = 0; q < pcntC; q++) outU[poffC + q] = srcC[q];
-			}
+			auto pixel_stores = [&]() {
+				bst128(rY, offY, u32x4{yl0.x, yl0.y, yl1.x, yl1.y});
+				bst64(rC, offC, cl0);
+				if (__ballot(pcntY | pcntC) != 0ull) {
+					for (uint32_t q = 0; q < pcntY; q++) outY[poffY + q] = srcY[q];
+					for (uint32_t q = 0; q < pcntC; q++) outU[poffC + q] = srcC[q];
+				}
+			};
+			// (round 5: issued after the publish instead, which the next wave waits on: +5.9 %, r05g -- the
+			// compiler then drains every outstanding store, vmcnt(0), at the top of each step)
+			pixel_stores();
 			if (lf_on) {
 				const bool last_row = r + 1 == R;
 				// tile row t of a column holds image row (MB row origin) + t - 4; rows >= 16 (luma) /
