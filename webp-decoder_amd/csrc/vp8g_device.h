@@ -107,6 +107,9 @@ inline size_t lds_bytes(int waves, uint32_t ctx_cols, bool global_ctx) {
 #ifndef VP8G_CHAIN_WPC
 #define VP8G_CHAIN_WPC 1
 #endif
+#ifndef VP8G_QUAD
+#define VP8G_QUAD 0
+#endif
 constexpr int kChainWaves = VP8G_CHAIN_NW;
 constexpr bool kChainG = VP8G_CHAIN_G != 0;
 constexpr int kChainWgPerCu = VP8G_CHAIN_WPC;
@@ -114,10 +117,22 @@ constexpr int kChainWgPerCu = VP8G_CHAIN_WPC;
 // interleaved, see pick_chain_interleave), or (global context) the cost sort's scratch of
 // kCostClasses + n_frames words
 inline size_t chain_ctx_lds(uint32_t ctx_cols, uint32_t n_frames, bool il = false) {
+	if (VP8G_QUAD) return (size_t)16 * (4 * kWht + 4 * 3 * kCtxBytesPerCol);  // (quads: the sort scratch sits in the wave areas)
 	return kChainG ? ((size_t)4 * (kCostClasses + n_frames) + 15) & ~(size_t)15
 	               : (il ? 4 : 2) * (size_t)ctx_cols * kCtxBytesPerCol;
 }
+// Experiment build VP8G_QUAD = 1: the chain decodes FOUR MB rows per wave
+// (vp8g_quad.inc).  A wave's LDS is four quarter areas (the half layout without the iWHT scratch)
+// and four 3-column context rings; the context between waves lives in device memory (the snapshot
+// buffer, one region per frame), so the chain's LDS no longer depends on the frame width.
+constexpr bool kChainQ = VP8G_QUAD != 0;
+constexpr int kQuarterBytes = kWht;                          // tile, borders, B_PRED buffers, residual park
+constexpr int kRingBytes = 3 * kCtxBytesPerCol;              // three MB columns of context
+constexpr int kQRings = kHdrBytes + 4 * kQuarterBytes;       // wave-relative: ring h at + h * kRingBytes
+constexpr int kQWaveBytes = 4 * kQuarterBytes + 4 * kRingBytes;
+constexpr int kQList = kHdrBytes + 16 * kQWaveBytes;         // the chain list (after 16 wave areas)
 inline size_t chain_lds_bytes(uint32_t ctx_cols, uint32_t list_max, uint32_t n_frames, bool il = false) {
+	if (kChainQ) return (size_t)kQList + 4 * (size_t)list_max;
 	return (size_t)kHdrBytes + (size_t)kChainWaves * kWaveBytes + chain_ctx_lds(ctx_cols, n_frames, il) + 4 * (size_t)list_max;
 }
 
@@ -182,6 +197,9 @@ bool pick_chain_split(uint32_t n_frames, uint32_t ctx_cols, uint32_t workgroups,
 // halves the chain's fill and drain.  Needs every frame of the batch the same size, four context
 // slots in LDS and no mirror split (VP8G_CHAIN_IL=0 / 1 forces it off / on where it fits).
 bool pick_chain_interleave(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint32_t ctx_cols, uint32_t workgroups, bool split);
+// (VP8G_QUAD builds) every frame of the batch can take the quad kernel (whole row pieces, no
+// loop-filter-only frames); the launch then needs `snap` (every frame's context) in any mode.
+bool quad_supported(const Vp8gFrameDesc* h_descs, uint32_t n_frames);
 // split: `snap` holds n_frames * ctx_cols * kCtxBytesPerCol bytes, `flags` n_frames words that hold
 // no value equal to `epoch` (a per-launch counter) before the launch.
 hipError_t launch_chain(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const Vp8gBatchArrays& arrays, uint8_t* d_out,

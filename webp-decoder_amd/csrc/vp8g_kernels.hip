@@ -1796,6 +1796,10 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 #endif
 }
 
+#if VP8G_QUAD
+#include "vp8g_quad.inc"
+#endif
+
 // The dynamic-LDS limit of a kernel instantiation, set once to the whole of the CU's LDS (the
 // kernel has no static LDS): concurrent launches from several threads then never race a smaller
 // value set by another thread between its own set and launch.
@@ -1937,12 +1941,25 @@ bool pick_chain_interleave(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint
 		const char* e = getenv("VP8G_CHAIN_IL");
 		return e ? atoi(e) : VP8G_CHAIN_IL_DEFAULT;
 	}();
-	if (mode == 0 || kChainG || split || workgroups == 0 || n_frames < 2 * workgroups) return false;
+	if (mode == 0 || (kChainG && !kChainQ) || split || workgroups == 0 || n_frames < 2 * workgroups) return false;
 	for (uint32_t i = 1; i < n_frames; i++)
 		if (h_descs[i].mb_cols != h_descs[0].mb_cols || h_descs[i].mb_rows != h_descs[0].mb_rows) return false;
 	if (h_descs[0].mb_rows < 2) return false;
 	const uint32_t list_max = (n_frames + workgroups - 1) / workgroups;
 	return (size_t)kChainWgPerCu * chain_lds_bytes(ctx_cols, list_max, n_frames, true) <= (size_t)kMaxLds;
+}
+
+bool quad_supported(const Vp8gFrameDesc* h_descs, uint32_t n_frames) {
+	// (VP8G_QUAD builds) whole 16-B / 8-B row pieces (frame_kernel's fl_fast; the planes' base is at
+	// least 16-B aligned), no loop-filter-only frames
+	for (uint32_t i = 0; i < n_frames; i++) {
+		const Vp8gFrameDesc& d = h_descs[i];
+		if (d.mb_cols == 0 || d.mb_rows == 0) continue;
+		if ((d.flags & VP8G_F_LF_ONLY) || d.width != 16u * d.mb_cols || ((d.out_y | d.stride_y) & 15u) != 0 ||
+		    ((d.out_u | d.stride_uv | (d.out_v - d.out_u)) & 7u) != 0)
+			return false;
+	}
+	return true;
 }
 
 hipError_t launch_chain(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const Vp8gBatchArrays& arrays, uint8_t* d_out,
@@ -1952,6 +1969,19 @@ hipError_t launch_chain(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const V
 	if ((split && (!snap || !flags)) || (kChainG && !snap) || (interleave && split)) return hipErrorInvalidValue;
 	const uint32_t list_max = (n_frames + workgroups - 1) / workgroups;
 	const size_t lds = chain_lds_bytes(ctx_cols, split ? 2 * list_max : list_max, n_frames, interleave);
+#if VP8G_QUAD
+	// (experiment build: four MB rows per wave; the snapshot buffer holds every frame's context)
+	if (!snap) return hipErrorInvalidValue;
+	{
+		static const hipError_t eq =
+		    hipFuncSetAttribute((const void*)quad_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLds);
+		if (eq != hipSuccess) return eq;
+		hipLaunchKernelGGL(quad_kernel<16>, dim3(workgroups), dim3(16 * 64), lds, stream, d_descs, arrays, d_out, ctx_cols, snap,
+		                   split ? epoch : 1u, split ? flags : nullptr, (ordered ? 1u : 0u) | (split ? 2u : 0u) | (interleave ? 4u : 0u),
+		                   n_frames);
+		return hipGetLastError();
+	}
+#endif
 	auto fn = frame_kernel<kChainWaves, kChainG, false, true>;
 	hipError_t e = lds_attr<kChainWaves, kChainG, false, true>();
 	if (e != hipSuccess) return e;

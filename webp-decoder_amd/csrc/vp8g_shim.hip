@@ -368,9 +368,11 @@ int run_locked(DevState& g_dev, const std::vector<Vp8gFrameDesc>& descs, const V
 		HIP_TRY(grow(g_dev, &g_dev.mbox, &g_dev.mbox_cap, mb + pb), "hipMalloc(mailbox)");
 	}
 	bool ordered = false;
-	const uint32_t wg = !big && !waves_hint ? vp8g::pick_chain(descs.data(), n, max_cols, &ordered) : 0u;
+	const uint32_t wg = !big && !waves_hint && (!vp8g::kChainQ || vp8g::quad_supported(descs.data(), n))
+	                        ? vp8g::pick_chain(descs.data(), n, max_cols, &ordered)
+	                        : 0u;
 	const bool split_want = wg && vp8g::pick_chain_split(n, max_cols, wg, ordered);
-	if (wg && vp8g::kChainG)  // (experiment builds: the chain's context in device memory, in the snapshot buffer)
+	if (wg && (vp8g::kChainG || vp8g::kChainQ))  // (experiment builds: the chain's context in device memory, in the snapshot buffer)
 		HIP_TRY(grow(g_dev, &g_dev.snap, &g_dev.snap_cap, (size_t)n * max_cols * vp8g::kCtxBytesPerCol), "hipMalloc(context)");
 	if (split_want) {
 		HIP_TRY(grow(g_dev, &g_dev.snap, &g_dev.snap_cap, (size_t)n * max_cols * vp8g::kCtxBytesPerCol), "hipMalloc(snapshots)");
