@@ -50,7 +50,7 @@ oracle:
 # Diagnostic variants of libvp8g (never loaded by the product path; select with VP8G_LIB=...):
 # per-phase shader-clock stamps, and phase ablations (timing only, wrong output).
 DIAG := $(LIB)/diag
-DIAG_VARIANTS := stamps abl1 abl2 abl4 abl8 abl15 abl16 quad
+DIAG_VARIANTS := stamps abl1 abl2 abl4 abl8 abl15 abl16 pairs
 diag: $(foreach v,$(DIAG_VARIANTS),$(DIAG)/libvp8g_$(v).so) $(DIAG)/libvp8g_stall.so
 $(DIAG):
 	mkdir -p $@
@@ -60,9 +60,9 @@ $(DIAG)/libvp8g_stamps.so: $(HIP_SRC) $(HIP_HDR) | $(DIAG)
 # (tests/test_gpu_batch.py: a stalled producer must end the launch promptly with EIO)
 $(DIAG)/libvp8g_stall.so: $(HIP_SRC) $(HIP_HDR) | $(DIAG)
 	$(HIPCC) $(HIPFLAGS) -DVP8G_WAIT_TICKS=2000000ull -DVP8G_TEST_STALL_WAVE=1 -shared -Wl,-Bsymbolic -o $@ $(HIP_SRC) -L$(LIB) -lvp8host -Wl,-rpath,'$$ORIGIN/..' -lpthread
-# experiment build: the chain with four MB rows per wave (csrc/vp8g_quad.inc)
-$(DIAG)/libvp8g_quad.so: $(HIP_SRC) $(HIP_HDR) $(PKG)/csrc/vp8g_quad.inc | $(DIAG)
-	$(HIPCC) $(HIPFLAGS) -DVP8G_QUAD=1 -shared -Wl,-Bsymbolic -o $@ $(HIP_SRC) -L$(LIB) -lvp8host -Wl,-rpath,'$$ORIGIN/..' -lpthread
+# A/B build: the chain with two MB rows per wave (frame_kernel) instead of the quad kernel
+$(DIAG)/libvp8g_pairs.so: $(HIP_SRC) $(HIP_HDR) | $(DIAG)
+	$(HIPCC) $(HIPFLAGS) -DVP8G_QUAD_DEFAULT=0 -shared -Wl,-Bsymbolic -o $@ $(HIP_SRC) -L$(LIB) -lvp8host -Wl,-rpath,'$$ORIGIN/..' -lpthread
 $(DIAG)/libvp8g_abl%.so: $(HIP_SRC) $(HIP_HDR) | $(DIAG)
 	$(HIPCC) $(HIPFLAGS) -DVP8G_ABLATE=$* -shared -Wl,-Bsymbolic -o $@ $(HIP_SRC) -L$(LIB) -lvp8host -Wl,-rpath,'$$ORIGIN/..' -lpthread
 

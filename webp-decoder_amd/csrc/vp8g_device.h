@@ -107,32 +107,28 @@ inline size_t lds_bytes(int waves, uint32_t ctx_cols, bool global_ctx) {
 #ifndef VP8G_CHAIN_WPC
 #define VP8G_CHAIN_WPC 1
 #endif
-#ifndef VP8G_QUAD
-#define VP8G_QUAD 0
-#endif
 constexpr int kChainWaves = VP8G_CHAIN_NW;
 constexpr bool kChainG = VP8G_CHAIN_G != 0;
 constexpr int kChainWgPerCu = VP8G_CHAIN_WPC;
 // LDS context area of a chain workgroup: the two context slots (four when two frames run
 // interleaved, see pick_chain_interleave), or (global context) the cost sort's scratch of
 // kCostClasses + n_frames words
-inline size_t chain_ctx_lds(uint32_t ctx_cols, uint32_t n_frames, bool il = false) {
-	if (VP8G_QUAD) return (size_t)16 * (4 * kWht + 4 * 3 * kCtxBytesPerCol);  // (quads: the sort scratch sits in the wave areas)
-	return kChainG ? ((size_t)4 * (kCostClasses + n_frames) + 15) & ~(size_t)15
-	               : (il ? 4 : 2) * (size_t)ctx_cols * kCtxBytesPerCol;
-}
-// Experiment build VP8G_QUAD = 1: the chain decodes FOUR MB rows per wave
-// (vp8g_quad.inc).  A wave's LDS is four quarter areas (the half layout without the iWHT scratch)
-// and four 3-column context rings; the context between waves lives in device memory (the snapshot
-// buffer, one region per frame), so the chain's LDS no longer depends on the frame width.
-constexpr bool kChainQ = VP8G_QUAD != 0;
+// Four MB rows per wave (the quad chain kernel, vp8g_quad.inc): a wave's LDS is four
+// quarter areas (the half layout without the iWHT scratch) and four 3-column context rings; the
+// context between waves lives in device memory (the snapshot buffer, one region per frame), so the
+// quad chain's LDS does not depend on the frame width.  Chosen per batch (pick_quad).
 constexpr int kQuarterBytes = kWht;                          // tile, borders, B_PRED buffers, residual park
 constexpr int kRingBytes = 3 * kCtxBytesPerCol;              // three MB columns of context
 constexpr int kQRings = kHdrBytes + 4 * kQuarterBytes;       // wave-relative: ring h at + h * kRingBytes
 constexpr int kQWaveBytes = 4 * kQuarterBytes + 4 * kRingBytes;
 constexpr int kQList = kHdrBytes + 16 * kQWaveBytes;         // the chain list (after 16 wave areas)
-inline size_t chain_lds_bytes(uint32_t ctx_cols, uint32_t list_max, uint32_t n_frames, bool il = false) {
-	if (kChainQ) return (size_t)kQList + 4 * (size_t)list_max;
+inline size_t chain_ctx_lds(uint32_t ctx_cols, uint32_t n_frames, bool il = false, bool quad = false) {
+	if (quad) return (size_t)16 * kQWaveBytes;  // (the cost sort's scratch sits in the wave areas)
+	return kChainG ? ((size_t)4 * (kCostClasses + n_frames) + 15) & ~(size_t)15
+	               : (il ? 4 : 2) * (size_t)ctx_cols * kCtxBytesPerCol;
+}
+inline size_t chain_lds_bytes(uint32_t ctx_cols, uint32_t list_max, uint32_t n_frames, bool il = false, bool quad = false) {
+	if (quad) return (size_t)kQList + 4 * (size_t)list_max;
 	return (size_t)kHdrBytes + (size_t)kChainWaves * kWaveBytes + chain_ctx_lds(ctx_cols, n_frames, il) + 4 * (size_t)list_max;
 }
 
@@ -188,23 +184,27 @@ uint32_t pick_order(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint32_t ns
 // Chain mode for n_frames frames on this device: the workgroup count (0 = not applicable: too few
 // frames, a context too wide for two LDS slots, or VP8G_CHAIN=0), and whether the frames are
 // placed by cost class (*ordered; needs the sort scratch to fit the context slots).
-uint32_t pick_chain(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint32_t ctx_cols, bool* ordered);
+uint32_t pick_chain(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint32_t ctx_cols, bool* ordered, bool quad = false);
 // Mirror split of a chain launch (vp8g_kernels.hip, kSegTop): worth it for ordered batches of at most
 // two frames per workgroup (VP8G_SPLITCHAIN=0 / 1 forces it off / on), and the doubled list must fit.
-bool pick_chain_split(uint32_t n_frames, uint32_t ctx_cols, uint32_t workgroups, bool ordered);
+bool pick_chain_split(uint32_t n_frames, uint32_t ctx_cols, uint32_t workgroups, bool ordered, bool quad = false);
 // Two-frame interleave of a chain launch (vp8g_kernels.hip): the frames of a workgroup's list run two
 // at a time with their MB row pairs alternating (the pair above is two global pairs back), which
 // halves the chain's fill and drain.  Needs every frame of the batch the same size, four context
 // slots in LDS and no mirror split (VP8G_CHAIN_IL=0 / 1 forces it off / on where it fits).
-bool pick_chain_interleave(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint32_t ctx_cols, uint32_t workgroups, bool split);
-// (VP8G_QUAD builds) every frame of the batch can take the quad kernel (whole row pieces, no
-// loop-filter-only frames); the launch then needs `snap` (every frame's context) in any mode.
+bool pick_chain_interleave(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint32_t ctx_cols, uint32_t workgroups, bool split,
+                           bool quad = false);
+// The quad chain kernel for this batch: every frame has whole 16-B / 8-B row pieces and is not
+// loop-filter-only (quad_supported), and VP8G_QUAD is not 0 (A/B experiments).  A quad launch needs
+// `snap` (every frame's context, n_frames * ctx_cols * kCtxBytesPerCol bytes) in every mode.
 bool quad_supported(const Vp8gFrameDesc* h_descs, uint32_t n_frames);
+bool pick_quad(const Vp8gFrameDesc* h_descs, uint32_t n_frames);
 // split: `snap` holds n_frames * ctx_cols * kCtxBytesPerCol bytes, `flags` n_frames words that hold
 // no value equal to `epoch` (a per-launch counter) before the launch.
 hipError_t launch_chain(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const Vp8gBatchArrays& arrays, uint8_t* d_out,
                         uint32_t ctx_cols, hipStream_t stream, uint32_t workgroups, bool ordered, bool split = false,
-                        uint8_t* snap = nullptr, uint32_t* flags = nullptr, uint32_t epoch = 0, bool interleave = false);
+                        uint8_t* snap = nullptr, uint32_t* flags = nullptr, uint32_t epoch = 0, bool interleave = false,
+                        bool quad = false);
 
 constexpr uint32_t kMaxSplit = 8;
 int device_cus();

@@ -1796,9 +1796,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 #endif
 }
 
-#if VP8G_QUAD
 #include "vp8g_quad.inc"
-#endif
 
 // The dynamic-LDS limit of a kernel instantiation, set once to the whole of the CU's LDS (the
 // kernel has no static LDS): concurrent launches from several threads then never race a smaller
@@ -1896,7 +1894,7 @@ uint32_t pick_order(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint32_t ns
 	return 0;  // uniform batch: the order would be the identity
 }
 
-uint32_t pick_chain(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint32_t ctx_cols, bool* ordered) {
+uint32_t pick_chain(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint32_t ctx_cols, bool* ordered, bool quad) {
 #ifndef VP8G_CHAIN_DEFAULT  // (A/B builds: -DVP8G_CHAIN_DEFAULT=0)
 #define VP8G_CHAIN_DEFAULT -1
 #endif
@@ -1910,16 +1908,17 @@ uint32_t pick_chain(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint32_t ct
 	const uint32_t slots = (uint32_t)n_cus * (uint32_t)kChainWgPerCu;
 	const uint32_t wg = n_frames < slots ? n_frames : slots;
 	const uint32_t list_max = (n_frames + wg - 1) / wg;
-	if (ctx_cols > 1024 || (size_t)kChainWgPerCu * chain_lds_bytes(ctx_cols, list_max, n_frames) > (size_t)kMaxLds) return 0;
+	if (ctx_cols > 1024 || (size_t)(quad ? 1 : kChainWgPerCu) * chain_lds_bytes(ctx_cols, list_max, n_frames, false, quad) > (size_t)kMaxLds)
+		return 0;
 	// cost-class placement when the classes differ and the sort scratch fits the context slots
 	const uint32_t c0 = cost_class(h_descs[0]);
 	bool differ = false;
 	for (uint32_t i = 1; i < n_frames && !differ; i++) differ = cost_class(h_descs[i]) != c0;
-	*ordered = differ && (size_t)4 * (kCostClasses + n_frames) <= chain_ctx_lds(ctx_cols, n_frames) && pick_order(h_descs, n_frames, 1) != 0;
+	*ordered = differ && (size_t)4 * (kCostClasses + n_frames) <= chain_ctx_lds(ctx_cols, n_frames, false, quad) && pick_order(h_descs, n_frames, 1) != 0;
 	return wg;
 }
 
-bool pick_chain_split(uint32_t n_frames, uint32_t ctx_cols, uint32_t workgroups, bool ordered) {
+bool pick_chain_split(uint32_t n_frames, uint32_t ctx_cols, uint32_t workgroups, bool ordered, bool quad) {
 #ifndef VP8G_SPLITCHAIN_DEFAULT  // (A/B builds: -DVP8G_SPLITCHAIN_DEFAULT=0 / 1)
 #define VP8G_SPLITCHAIN_DEFAULT -1
 #endif
@@ -1929,11 +1928,12 @@ bool pick_chain_split(uint32_t n_frames, uint32_t ctx_cols, uint32_t workgroups,
 	}();
 	if (mode == 0 || workgroups == 0) return false;
 	const uint32_t list_max = (n_frames + workgroups - 1) / workgroups;
-	if ((size_t)kChainWgPerCu * chain_lds_bytes(ctx_cols, 2 * list_max, n_frames) > (size_t)kMaxLds) return false;
+	if ((size_t)(quad ? 1 : kChainWgPerCu) * chain_lds_bytes(ctx_cols, 2 * list_max, n_frames, false, quad) > (size_t)kMaxLds) return false;
 	return mode > 0 || (ordered && list_max <= 2);
 }
 
-bool pick_chain_interleave(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint32_t ctx_cols, uint32_t workgroups, bool split) {
+bool pick_chain_interleave(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint32_t ctx_cols, uint32_t workgroups, bool split,
+                           bool quad) {
 #ifndef VP8G_CHAIN_IL_DEFAULT  // (A/B builds: -DVP8G_CHAIN_IL_DEFAULT=0)
 #define VP8G_CHAIN_IL_DEFAULT -1
 #endif
@@ -1941,17 +1941,17 @@ bool pick_chain_interleave(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint
 		const char* e = getenv("VP8G_CHAIN_IL");
 		return e ? atoi(e) : VP8G_CHAIN_IL_DEFAULT;
 	}();
-	if (mode == 0 || (kChainG && !kChainQ) || split || workgroups == 0 || n_frames < 2 * workgroups) return false;
+	if (mode == 0 || (kChainG && !quad) || split || workgroups == 0 || n_frames < 2 * workgroups) return false;
 	for (uint32_t i = 1; i < n_frames; i++)
 		if (h_descs[i].mb_cols != h_descs[0].mb_cols || h_descs[i].mb_rows != h_descs[0].mb_rows) return false;
 	if (h_descs[0].mb_rows < 2) return false;
 	const uint32_t list_max = (n_frames + workgroups - 1) / workgroups;
-	return (size_t)kChainWgPerCu * chain_lds_bytes(ctx_cols, list_max, n_frames, true) <= (size_t)kMaxLds;
+	return (size_t)(quad ? 1 : kChainWgPerCu) * chain_lds_bytes(ctx_cols, list_max, n_frames, true, quad) <= (size_t)kMaxLds;
 }
 
 bool quad_supported(const Vp8gFrameDesc* h_descs, uint32_t n_frames) {
-	// (VP8G_QUAD builds) whole 16-B / 8-B row pieces (frame_kernel's fl_fast; the planes' base is at
-	// least 16-B aligned), no loop-filter-only frames
+	// whole 16-B / 8-B row pieces (frame_kernel's fl_fast; the output base is at least 16-B aligned), no
+	// loop-filter-only frames
 	for (uint32_t i = 0; i < n_frames; i++) {
 		const Vp8gFrameDesc& d = h_descs[i];
 		if (d.mb_cols == 0 || d.mb_rows == 0) continue;
@@ -1962,17 +1962,26 @@ bool quad_supported(const Vp8gFrameDesc* h_descs, uint32_t n_frames) {
 	return true;
 }
 
+bool pick_quad(const Vp8gFrameDesc* h_descs, uint32_t n_frames) {
+#ifndef VP8G_QUAD_DEFAULT  // (A/B builds: -DVP8G_QUAD_DEFAULT=0, the two-rows-per-wave chain)
+#define VP8G_QUAD_DEFAULT 1
+#endif
+	static const int mode = [] {  // VP8G_QUAD=0: never (A/B experiments)
+		const char* e = getenv("VP8G_QUAD");
+		return e ? atoi(e) : VP8G_QUAD_DEFAULT;
+	}();
+	return mode != 0 && quad_supported(h_descs, n_frames);
+}
+
 hipError_t launch_chain(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const Vp8gBatchArrays& arrays, uint8_t* d_out,
                         uint32_t ctx_cols, hipStream_t stream, uint32_t workgroups, bool ordered, bool split, uint8_t* snap,
-                        uint32_t* flags, uint32_t epoch, bool interleave) {
+                        uint32_t* flags, uint32_t epoch, bool interleave, bool quad) {
 	if (n_frames == 0) return hipSuccess;
 	if ((split && (!snap || !flags)) || (kChainG && !snap) || (interleave && split)) return hipErrorInvalidValue;
 	const uint32_t list_max = (n_frames + workgroups - 1) / workgroups;
-	const size_t lds = chain_lds_bytes(ctx_cols, split ? 2 * list_max : list_max, n_frames, interleave);
-#if VP8G_QUAD
-	// (experiment build: four MB rows per wave; the snapshot buffer holds every frame's context)
-	if (!snap) return hipErrorInvalidValue;
-	{
+	const size_t lds = chain_lds_bytes(ctx_cols, split ? 2 * list_max : list_max, n_frames, interleave, quad);
+	if (quad) {  // four MB rows per wave; the snapshot buffer holds every frame's context
+		if (!snap) return hipErrorInvalidValue;
 		static const hipError_t eq =
 		    hipFuncSetAttribute((const void*)quad_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLds);
 		if (eq != hipSuccess) return eq;
@@ -1981,7 +1990,6 @@ hipError_t launch_chain(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const V
 		                   n_frames);
 		return hipGetLastError();
 	}
-#endif
 	auto fn = frame_kernel<kChainWaves, kChainG, false, true>;
 	hipError_t e = lds_attr<kChainWaves, kChainG, false, true>();
 	if (e != hipSuccess) return e;

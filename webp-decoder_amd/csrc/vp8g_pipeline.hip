@@ -702,7 +702,7 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 					PTRY(hipGetLastError(), "expand launch");
 				}
 				bool ordered = false;
-				const uint32_t wg = big || k > 1 || vp8g::kChainG || vp8g::kChainQ ? 0u : vp8g::pick_chain(s.descs.data(), nf, max_cols, &ordered);
+				const uint32_t wg = big || k > 1 || vp8g::kChainG ? 0u : vp8g::pick_chain(s.descs.data(), nf, max_cols, &ordered);
 				if (wg)  // more frames than CUs: one 16-wave chain of frames per CU
 					PTRY(vp8g::launch_chain((const Vp8gFrameDesc*)(d + L.desc), nf, arr, d + L.out, max_cols, stream, wg, ordered),
 					     "recon launch");

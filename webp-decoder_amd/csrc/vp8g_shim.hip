@@ -368,11 +368,10 @@ int run_locked(DevState& g_dev, const std::vector<Vp8gFrameDesc>& descs, const V
 		HIP_TRY(grow(g_dev, &g_dev.mbox, &g_dev.mbox_cap, mb + pb), "hipMalloc(mailbox)");
 	}
 	bool ordered = false;
-	const uint32_t wg = !big && !waves_hint && (!vp8g::kChainQ || vp8g::quad_supported(descs.data(), n))
-	                        ? vp8g::pick_chain(descs.data(), n, max_cols, &ordered)
-	                        : 0u;
-	const bool split_want = wg && vp8g::pick_chain_split(n, max_cols, wg, ordered);
-	if (wg && (vp8g::kChainG || vp8g::kChainQ))  // (experiment builds: the chain's context in device memory, in the snapshot buffer)
+	const bool quad = !big && !waves_hint && vp8g::pick_quad(descs.data(), n);  // (four MB rows per wave)
+	const uint32_t wg = !big && !waves_hint ? vp8g::pick_chain(descs.data(), n, max_cols, &ordered, quad) : 0u;
+	const bool split_want = wg && vp8g::pick_chain_split(n, max_cols, wg, ordered, quad);
+	if (wg && (vp8g::kChainG || quad))  // (experiment builds: the chain's context in device memory, in the snapshot buffer)
 		HIP_TRY(grow(g_dev, &g_dev.snap, &g_dev.snap_cap, (size_t)n * max_cols * vp8g::kCtxBytesPerCol), "hipMalloc(context)");
 	if (split_want) {
 		HIP_TRY(grow(g_dev, &g_dev.snap, &g_dev.snap_cap, (size_t)n * max_cols * vp8g::kCtxBytesPerCol), "hipMalloc(snapshots)");
@@ -403,9 +402,9 @@ int run_locked(DevState& g_dev, const std::vector<Vp8gFrameDesc>& descs, const V
 			HIP_TRY(hipMemsetAsync(g_dev.sflags, 0, g_dev.sflags_cap, s), "memset(flags)");
 		}
 		crossed = split;
-		const bool il = vp8g::pick_chain_interleave(descs.data(), n, max_cols, wg, split);  // (1080p batches: two frames interleaved)
+		const bool il = vp8g::pick_chain_interleave(descs.data(), n, max_cols, wg, split, quad);  // (1080p batches: two frames interleaved)
 		HIP_TRY(vp8g::launch_chain((const Vp8gFrameDesc*)d_descs, n, arr, d_out, max_cols, s, wg, ordered, split, g_dev.snap,
-		                           (uint32_t*)g_dev.sflags, g_dev.epoch, il),
+		                           (uint32_t*)g_dev.sflags, g_dev.epoch, il, quad),
 		        "launch");
 	} else {
 		const uint32_t ord = vp8g::pick_order(descs.data(), n, 1);  // cost-balanced placement (vp8g_device.h)
