@@ -42,7 +42,7 @@ traces = glob.glob(str(src / "trace" / "**" / "*kernel_trace.csv"), recursive=Tr
 if traces and bench_line:
     durs = []
     for r in csv.DictReader(open(traces[0])):
-        if "frame_kernel" in r["Kernel_Name"]:
+        if ("frame_kernel" in r["Kernel_Name"] or "quad_kernel" in r["Kernel_Name"]):
             durs.append((int(r["Start_Timestamp"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6))
     durs = [d for _, d in sorted(durs)]
     warm = durs[1:]
@@ -69,7 +69,7 @@ def per_dispatch(counter):
     f = glob.glob(str(src / f"pmc_{counter}" / "**" / "*counter_collection.csv"), recursive=True)[0]
     tot, disp = 0.0, set()
     for r in csv.DictReader(open(f)):
-        if "frame_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+        if ("frame_kernel" in r["Kernel_Name"] or "quad_kernel" in r["Kernel_Name"]) and r["Counter_Name"] == counter:
             tot += float(r["Counter_Value"])
             disp.add(r["Dispatch_Id"])
     return tot / len(disp), len(disp)
