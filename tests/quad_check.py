@@ -1,0 +1,64 @@
+"""Batch decoded by the quad chain kernel (csrc/vp8g_quad.inc: four MB rows per wave; chosen for
+batches of whole-piece frames), every slot against the oracle.  Imported by tests/test_gpu_quad.py,
+and run as a child process there when an environment switch read once by libvp8g must be set
+(VP8G_SPLITCHAIN=1: every frame of more than four MB rows split between two workgroups).
+
+Frames: widths multiples of 16 (whole 16-B / 8-B row pieces), heights giving 1..19 MB rows -- last
+quads of one, two, three and four rows -- and odd pixel heights (cropped bottom rows), all synthetic
+profiles (segments, loop-filter deltas, simple and normal filter, +-2114 coefficients), filtered and
+unfiltered, in a scrambled order with one slot in eight left empty."""
+import pathlib
+import sys
+
+import numpy as np
+import torch
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "webp-decoder_amd"))
+import vp8g  # noqa: E402
+import vp8g_batch  # noqa: E402
+
+SIZES = [(16, 16), (16, 48), (32, 24), (160, 64), (48, 112), (1024, 80), (160, 96), (64, 200), (128, 304), (96, 36)]
+
+
+def run(n=1800, seed=0x0A4D, launches=1):
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(seed)
+    frames = [vp8g.synth_frame(*SIZES[i % len(SIZES)], seed ^ (i * 0x9E37), profile=i % 3) for i in range(40)]
+    W = max(w for w, _ in SIZES)
+    H = max(h for _, h in SIZES)
+    b = vp8g_batch.DeviceBatch(n, W, H, dev)
+    b.out.fill_(0xA5)
+    pick = rng.integers(0, len(frames), n)
+    empty = set(rng.choice(n, n // 8, replace=False).tolist())
+    for i in range(n):
+        if i not in empty:
+            b.place(i, frames[pick[i]], bool(pick[i] % 2))
+    b.commit()
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    for _ in range(launches):
+        b.launch(stream)
+        torch.cuda.synchronize()
+        if b.status_word() != 0:
+            return [f"status {b.status_word()}"]
+    exp, bad = {}, []
+    for i in range(n):
+        if i in empty:
+            continue
+        j = int(pick[i])
+        key = (j, bool(j % 2))
+        if key not in exp:
+            exp[key] = vp8g.oracle_reconstruct(frames[j], bool(j % 2))
+        if b.frame_output(i)[:len(exp[key])] != exp[key]:
+            bad.append(i)
+    for i in sorted(empty)[:16]:
+        if b.frame_output(i) != b"\xa5" * b.i420:
+            bad.append(f"empty slot {i} written")
+    for f in frames:
+        f.free()
+    return bad
+
+
+if __name__ == "__main__":
+    bad = run(launches=2)
+    print("OK" if not bad else f"BAD {len(bad)}: {bad[:8]}")

@@ -1,0 +1,63 @@
+"""GPU: the quad chain kernel (csrc/vp8g_quad.inc) -- four MB rows per wave, the
+row above a quad handed over through device memory, progress published one step late -- on the
+shapes the bench batches do not have.  Reference path: src/m06_recon/vp8_recon.c:444-684 (MB
+driver) + src/m07_loopfilter/vp8_loopfilter.c:214-280 (filter order), per frame."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def test_quad_chain_mixed_whole_piece_frames(vp8g):
+    """1 800 slots (~7 frames per workgroup) of 40 distinct whole-piece frames, 1..19 MB rows (last
+    quads of 1, 2, 3 and 4 rows), cropped heights, filtered and unfiltered, one slot in eight empty:
+    every decoded slot equals the oracle's output, the empty slots stay untouched."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import quad_check
+    bad = quad_check.run()
+    assert not bad, f"{len(bad)} slots differ, e.g. {bad[:8]}"
+
+
+def test_quad_chain_mirror_split_forced(vp8g):
+    """The same kind of batch with the mirror split forced (VP8G_SPLITCHAIN=1, child process): a
+    bottom segment's first quad reads the frame's context from device memory after the top
+    segment's flag; two launches (the flags' epoch advances)."""
+    env = dict(os.environ, VP8G_SPLITCHAIN="1")
+    r = subprocess.run([sys.executable, str(ROOT / "tests" / "quad_check.py")], capture_output=True, text=True, timeout=240,
+                       env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip().endswith("OK"), r.stdout
+
+
+def test_quad_and_pairs_chains_agree(vp8g):
+    """260 x 4K fixtures (slot i <- fixture i % 4) through the quad chain and, in a child process with
+    VP8G_QUAD=0, through the two-rows-per-wave chain: both equal the reference's digests."""
+    code = r"""
+import json, pathlib, sys
+root = pathlib.Path(sys.argv[1])
+sys.path.insert(0, str(root / "webp-decoder_amd"))
+import torch, vp8g, vp8g_batch
+UHD = ["big/uhd_a_normal_seg4.webp", "big/uhd_b_simple_sharp3.webp", "big/uhd_c_normal_sharp6_seg1.webp",
+       "big/uhd_d_normal_q90.webp"]
+golden = json.loads((root / "tests" / "golden" / "digests.json").read_text())
+dev = torch.device("cuda:0")
+frames = [vp8g.decode_file(root / "tests" / "fixtures" / r) for r in UHD]
+b = vp8g_batch.DeviceBatch(260, 3840, 2160, dev)
+b.replicate(frames, True)
+b.commit()
+stream = torch.cuda.current_stream(dev).cuda_stream
+b.launch(stream)
+dig = b.digests(stream)
+bad = [i for i in range(260) if int(dig[i]) != int(golden["fixtures"][UHD[i % 4]]["yuvf"], 16)]
+print("OK" if not bad and b.status_word() == 0 else f"BAD {bad[:8]} status {b.status_word()}")
+"""
+    for env_extra in ({}, {"VP8G_QUAD": "0"}):
+        env = dict(os.environ, **env_extra)
+        r = subprocess.run([sys.executable, "-c", code, str(ROOT)], capture_output=True, text=True, timeout=240, env=env)
+        assert r.returncode == 0, (env_extra, r.stderr[-2000:])
+        assert r.stdout.strip().endswith("OK"), (env_extra, r.stdout)
