@@ -602,7 +602,9 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 			L.jobs = o, o = al256(o + (ctok ? nf * sizeof(Vp8gTokFrame) : 0));
 			L.desc = o, o = al256(o + nf * sizeof(Vp8gFrameDesc));
 			L.status = o, o = al256(o + 4);
-			L.gctx = o, o = al256(o + (big ? (uint64_t)nf * max_cols * vp8g::kCtxBytesPerCol : 0));
+			// (every frame's column context: the global-context variant for frames too wide for LDS, and
+			// the quad chain kernel, whose rows hand over through device memory)
+			L.gctx = o, o = al256(o + (uint64_t)nf * max_cols * vp8g::kCtxBytesPerCol);
 			L.mbox = o, o = al256(o + (k_plan > 1 ? (uint64_t)nf * k_plan * max_cols * vp8g::kCtxBytesPerCol : 0));
 			L.gprog = o, o = al256(o + (k_plan > 1 ? (uint64_t)nf * k_plan * 4 : 0));
 			L.out = o, o = al256(o + outb);
@@ -702,9 +704,11 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 					PTRY(hipGetLastError(), "expand launch");
 				}
 				bool ordered = false;
-				const uint32_t wg = big || k > 1 || vp8g::kChainG ? 0u : vp8g::pick_chain(s.descs.data(), nf, max_cols, &ordered);
+				const bool quad = !big && k == 1 && vp8g::pick_quad(s.descs.data(), nf);  // (four MB rows per wave)
+				const uint32_t wg = big || k > 1 || (vp8g::kChainG && !quad) ? 0u : vp8g::pick_chain(s.descs.data(), nf, max_cols, &ordered, quad);
 				if (wg)  // more frames than CUs: one 16-wave chain of frames per CU
-					PTRY(vp8g::launch_chain((const Vp8gFrameDesc*)(d + L.desc), nf, arr, d + L.out, max_cols, stream, wg, ordered),
+					PTRY(vp8g::launch_chain((const Vp8gFrameDesc*)(d + L.desc), nf, arr, d + L.out, max_cols, stream, wg, ordered, false,
+					                        quad ? d + L.gctx : nullptr, nullptr, 0u, false, quad),
 					     "recon launch");
 				else
 					PTRY(vp8g::launch_frames((const Vp8gFrameDesc*)(d + L.desc), nf, arr, d + L.out, max_cols, max_rows,
