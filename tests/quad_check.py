@@ -21,7 +21,7 @@ import vp8g_batch  # noqa: E402
 SIZES = [(16, 16), (16, 48), (32, 24), (160, 64), (48, 112), (1024, 80), (160, 96), (64, 200), (128, 304), (96, 36)]
 
 
-def run(n=1800, seed=0x0A4D, launches=1):
+def run(n=1800, seed=0x0A4D, launches=1, want_split=False):
     dev = torch.device("cuda:0")
     rng = np.random.default_rng(seed)
     frames = [vp8g.synth_frame(*SIZES[i % len(SIZES)], seed ^ (i * 0x9E37), profile=i % 3) for i in range(40)]
@@ -41,6 +41,9 @@ def run(n=1800, seed=0x0A4D, launches=1):
         torch.cuda.synchronize()
         if b.status_word() != 0:
             return [f"status {b.status_word()}"]
+        mode = b.launch_mode()
+        if not (mode & vp8g.MODE_CHAIN and mode & vp8g.MODE_QUAD) or (want_split and not mode & vp8g.MODE_MIRROR_SPLIT):
+            return [f"launch mode {mode}: not the quad chain{' with the mirror split' if want_split else ''}"]
     exp, bad = {}, []
     for i in range(n):
         if i in empty:
@@ -60,5 +63,6 @@ def run(n=1800, seed=0x0A4D, launches=1):
 
 
 if __name__ == "__main__":
-    bad = run(launches=2)
+    import os
+    bad = run(launches=2, want_split=os.environ.get("VP8G_SPLITCHAIN") == "1")
     print("OK" if not bad else f"BAD {len(bad)}: {bad[:8]}")

@@ -238,6 +238,8 @@ def test_device_batch_512_uhd_bench_launch(vp8g, digests):
     0's shard of BASELINE configs[3] / [4]): the chain kernel with the mirror split, every slot."""
     b, bad = run_batch(vp8g, UHD, 512, True, digests, slot0=0)
     assert not bad, f"{len(bad)} of 512 slots differ, e.g. {bad[:8]}"
+    mode = b.launch_mode()  # (the quad chain with the mirror split, as bench.py's launch)
+    assert mode & vp8g.MODE_CHAIN and mode & vp8g.MODE_QUAD and mode & vp8g.MODE_MIRROR_SPLIT, mode
     del b
     torch.cuda.empty_cache()
 
@@ -325,10 +327,14 @@ def test_chain_two_frame_interleave(vp8g, w, h):
     their MB row pairs alternating, four LDS context slots; chosen for batches of one frame size with at
     least two frames per workgroup, pick_chain_interleave): 549 distinct synthetic frames, so workgroups
     hold two or three frames (an odd last frame runs alone); 176x80 has an odd MB row count (the last
-    pair of every frame is a single row).  Every slot against the oracle."""
+    pair of every frame is a single row).  Every slot against the oracle; the launch mode read back
+    (vp8g_last_launch_mode) must be the interleaved chain."""
     import vp8g_batch
     dev = torch.device("cuda:0")
-    n = 549
+    # (two frames per workgroup and, for every seventh, a third: derived from the CU count, so the
+    # interleave -- it needs at least two frames per workgroup -- is chosen on any part; ADVICE r04)
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    n = 2 * cus + cus // 7
     b = vp8g_batch.DeviceBatch(n, w, h, dev)
     frames = [vp8g.synth_frame(w, h, 0x1A7E ^ i, profile=i % 3) for i in range(n)]
     for i, f in enumerate(frames):
@@ -338,6 +344,8 @@ def test_chain_two_frame_interleave(vp8g, w, h):
     b.launch(stream)
     torch.cuda.synchronize()
     assert b.status_word() == 0
+    mode = b.launch_mode()
+    assert mode & vp8g.MODE_CHAIN and mode & vp8g.MODE_INTERLEAVE, mode
     bad = [i for i, f in enumerate(frames) if b.frame_output(i) != vp8g.oracle_reconstruct(f, bool(i % 5))]
     assert not bad, f"{len(bad)} of {n} slots differ, e.g. {bad[:8]}"
     for f in frames:

@@ -54,10 +54,13 @@ stream = torch.cuda.current_stream(dev).cuda_stream
 b.launch(stream)
 dig = b.digests(stream)
 bad = [i for i in range(260) if int(dig[i]) != int(golden["fixtures"][UHD[i % 4]]["yuvf"], 16)]
-print("OK" if not bad and b.status_word() == 0 else f"BAD {bad[:8]} status {b.status_word()}")
+mode = b.launch_mode()
+print(mode, "OK" if not bad and b.status_word() == 0 else f"BAD {bad[:8]} status {b.status_word()}")
 """
     for env_extra in ({}, {"VP8G_QUAD": "0"}):
         env = dict(os.environ, **env_extra)
         r = subprocess.run([sys.executable, "-c", code, str(ROOT)], capture_output=True, text=True, timeout=240, env=env)
         assert r.returncode == 0, (env_extra, r.stderr[-2000:])
         assert r.stdout.strip().endswith("OK"), (env_extra, r.stdout)
+        mode = int(r.stdout.split()[0])
+        assert mode & vp8g.MODE_CHAIN and bool(mode & vp8g.MODE_QUAD) == (not env_extra), (env_extra, mode)

@@ -24,6 +24,8 @@
 namespace {
 
 thread_local char g_err[256];
+// launch mode of the calling thread's last reconstruction launch (vp8g_last_launch_mode)
+thread_local uint32_t g_mode = 0;
 
 void set_err(const char* where, hipError_t e) {
 	snprintf(g_err, sizeof(g_err), "%s: %s", where, hipGetErrorString(e));
@@ -188,6 +190,7 @@ std::atomic<size_t> g_held{0};
 
 vp8g::GateScope::GateScope(hipStream_t s) : s_(s) {
 	g_gate.mu.lock();
+	const hipError_t before = hipPeekAtLastError();  // (a caller's pending error stays for the caller)
 	if (g_gate.xpending) {
 		const hipError_t q = hipEventQuery(g_gate.xev);
 		if (q == hipSuccess) g_gate.xpending = false;
@@ -199,7 +202,9 @@ vp8g::GateScope::GateScope(hipStream_t s) : s_(s) {
 		if (hipEventQuery(x.ev) == hipSuccess) x.live = false;
 		else may_cross_ = false;  // in flight (or unknown): no cross-workgroup launch beside it
 	}
-	(void)hipGetLastError();  // (hipErrorNotReady of the queries must not read as a launch failure later)
+	// (hipErrorNotReady of the queries must not read as a launch failure later; an error that was
+	// pending before them is left alone)
+	if (before == hipSuccess || hipPeekAtLastError() == hipErrorNotReady) (void)hipGetLastError();
 }
 
 vp8g::GateScope::~GateScope() { g_gate.mu.unlock(); }
@@ -245,16 +250,31 @@ void release_buffers(DevState& g) {
 	}
 }
 void trim_idle(const DevState* keep) {
-	std::lock_guard<std::mutex> lk(g_pool.mu);
+	// The idle contexts are taken (marked busy) under the pool lock and released outside it: waiting
+	// for their last asynchronous launch and hipFree (which synchronises the device) must not block
+	// every other thread's lease for the length of a batch.
+	bool took[kMaxCtx] = {};
+	{
+		std::lock_guard<std::mutex> lk(g_pool.mu);
+		for (int i = 0; i < kMaxCtx; i++) {
+			const DevState& o = g_pool.ctx[i];
+			if (g_pool.busy[i] || &o == keep || !o.ready) continue;
+			g_pool.busy[i] = took[i] = true;
+		}
+	}
 	for (int i = 0; i < kMaxCtx; i++) {
+		if (!took[i]) continue;
 		DevState& o = g_pool.ctx[i];
-		if (g_pool.busy[i] || &o == keep || !o.ready) continue;
 		if (o.pending) {
 			if (hipEventSynchronize(o.done) != hipSuccess) continue;
 			o.pending = false;
 		}
 		release_buffers(o);
 	}
+	std::lock_guard<std::mutex> lk(g_pool.mu);
+	for (int i = 0; i < kMaxCtx; i++)
+		if (took[i]) g_pool.busy[i] = false;
+	g_pool.cv.notify_all();
 }
 hipError_t grow(DevState& g, uint8_t** p, size_t* cap, size_t need) {
 	if (need <= *cap) return hipSuccess;
@@ -346,7 +366,9 @@ int run_locked(DevState& g_dev, const std::vector<Vp8gFrameDesc>& descs, const V
 	}
 	const uint32_t env = split_env();
 	// Buffers for every mode this call could pick, before the gate (growing may wait for this context's
-	// previous launch, or release idle contexts' buffers).
+	// previous launch, or release idle contexts' buffers).  A call that the gate then keeps from the
+	// cross-workgroup modes (another launch in flight) holds mailbox / snapshot memory it did not use
+	// this time: the price of never allocating inside the gate, bounded by trim_idle.
 	uint32_t nw = vp8g::pick_waves(waves_hint, max_rows, n);
 	const bool try_split = (may_split || env > 1) && env != 1 && !waves_hint;
 	const uint32_t nw_split = try_split && vp8g::pick_split(env, n, 8, max_rows) > 1 ? 8u : nw;
@@ -388,6 +410,7 @@ int run_locked(DevState& g_dev, const std::vector<Vp8gFrameDesc>& descs, const V
 	// frame: 8 waves x 8 parts 3.9 ms per call, 16 waves x 1..8 parts 8.1..4.7 ms)
 	const uint32_t k = alone && k_want > 1 ? k_want : 1u;
 	bool crossed = k > 1;
+	g_mode = k > 1 ? VP8G_MODE_SPLIT_PARTS : 0u;
 	if (k > 1) {
 		const size_t mb = (size_t)n * k * max_cols * vp8g::kCtxBytesPerCol, pb = (size_t)n * k * sizeof(uint32_t);
 		HIP_TRY(hipMemsetAsync(g_dev.mbox + mb, 0, pb, s), "memset(progress)");
@@ -403,6 +426,7 @@ int run_locked(DevState& g_dev, const std::vector<Vp8gFrameDesc>& descs, const V
 		}
 		crossed = split;
 		const bool il = vp8g::pick_chain_interleave(descs.data(), n, max_cols, wg, split, quad);  // (1080p batches: two frames interleaved)
+		g_mode = VP8G_MODE_CHAIN | (split ? VP8G_MODE_MIRROR_SPLIT : 0u) | (il ? VP8G_MODE_INTERLEAVE : 0u) | (quad ? VP8G_MODE_QUAD : 0u);
 		HIP_TRY(vp8g::launch_chain((const Vp8gFrameDesc*)d_descs, n, arr, d_out, max_cols, s, wg, ordered, split, g_dev.snap,
 		                           (uint32_t*)g_dev.sflags, g_dev.epoch, il, quad),
 		        "launch");
@@ -711,6 +735,8 @@ VP8G_API int vp8_loopfilter_apply_keyframe(Yuv420Image* img, const Vp8DecodedFra
 }
 
 VP8G_API const char* vp8g_last_error(void) { return g_err; }
+
+VP8G_API uint32_t vp8g_last_launch_mode(void) { return g_mode; }
 
 void vp8g::set_error_text(const char* where, hipError_t e) { set_err(where, e); }
 

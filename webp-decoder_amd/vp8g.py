@@ -221,6 +221,10 @@ def host_lib():
     return lib
 
 
+# vp8g_last_launch_mode bits (include/vp8g.h)
+MODE_CHAIN, MODE_MIRROR_SPLIT, MODE_INTERLEAVE, MODE_QUAD, MODE_SPLIT_PARTS = 1, 2, 4, 8, 16
+
+
 def gpu_lib():
     """libvp8g.so: the product path.  Raises if it is not built."""
     lib = _load("gpu", pathlib.Path(os.environ.get("VP8G_LIB", LIB_DIR / "libvp8g.so")))
@@ -244,6 +248,7 @@ def gpu_lib():
         lib.vp8g_reconstruct_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int, P(Yuv420Image)]
         lib.vp8g_last_error.restype = C.c_char_p
         lib.vp8g_abi_version.restype = C.c_uint32
+        lib.vp8g_last_launch_mode.restype = C.c_uint32
         lib.yuv420_write_ppm_fd.argtypes = [C.c_int, P(Yuv420Image)]
         lib.yuv420_write_png_fd.argtypes = [C.c_int, P(Yuv420Image)]
         lib.vp8g_encoded_size.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32]

@@ -116,6 +116,10 @@ class DeviceBatch:
         torch.cuda.synchronize(self.dev)
         return self.digest_buf.cpu().numpy().view(np.uint64).copy()
 
+    def launch_mode(self) -> int:
+        """VP8G_MODE_* bits of this thread's last launch (include/vp8g.h vp8g_last_launch_mode)."""
+        return int(vp8g.gpu_lib().vp8g_last_launch_mode())
+
     def status_word(self) -> int:
         return int(self.status[0].item())
 
