@@ -19,7 +19,7 @@ lines = open(out).read().split("\n")
 sym = None
 for l in lines:
     # NW, or a mangled template-argument fragment such as 16ELb0ELb0ELb1 (the chain kernel)
-    m = re.match(r"^(_ZN\S*frame_kernelILi%s\S*):\s*(;.*)?$" % (nw if "E" in nw else nw + "ELb0ELb0ELb0"), l)
+    m = re.match(r"^(_ZN\S*quad_kernelILi16\S*):\s*(;.*)?$", l) if nw == "quad" else re.match(r"^(_ZN\S*frame_kernelILi%s\S*):\s*(;.*)?$" % (nw if "E" in nw else nw + "ELb0ELb0ELb0"), l)
     if m:
         sym = m.group(1)
         break
