@@ -1,11 +1,11 @@
 #!/usr/bin/env python3
 """Per-MB instruction / wait / LDS summary of a tools/pmc_pass.sh run of the bench kernel, as the
-committed profiles/<tag>_frame_kernel_pmc.json (DESIGN.md §5 takes its numbers from it).
+committed profiles/<tag>_<kernel>_pmc.json (default kernel: quad_kernel, the bench's chain) (DESIGN.md §5 takes its numbers from it).
   tools/pmc_json.py <pmc dir> <tag> <build> [kernel filter]"""
 import collections, csv, glob, json, pathlib, sys
 
 d, tag, build = sys.argv[1], sys.argv[2], sys.argv[3]
-filt = sys.argv[4] if len(sys.argv) > 4 else "frame_kernel"
+filt = sys.argv[4] if len(sys.argv) > 4 else "quad_kernel"
 c = {}
 kname = None
 for f in sorted(glob.glob(d + "/pmc*/pmc_counter_collection.csv")):
@@ -35,6 +35,6 @@ out = {
     "lds": {"bank_conflict_share": round(c["SQ_LDS_BANK_CONFLICT"] / c["SQ_LDS_IDX_ACTIVE"], 3)},
     "valu_per_simd": round(c["SQ_INSTS_VALU"] / 1024),
 }
-p = pathlib.Path(__file__).resolve().parents[1] / "profiles" / f"{tag}_frame_kernel_pmc.json"
+p = pathlib.Path(__file__).resolve().parents[1] / "profiles" / f"{tag}_{filt}_pmc.json"
 p.write_text(json.dumps(out, indent=1) + "\n")
 print(p, json.dumps(out["per_mb"]), out["wave_time_shares"], out["lds"])

@@ -18,7 +18,7 @@ for i, lib in libs:
     f = glob.glob(str(src / f"mix{i}" / "**" / "*counter_collection.csv"), recursive=True)[0]
     tot, disp = {}, {}
     for r in csv.DictReader(open(f)):
-        if "frame_kernel" not in r["Kernel_Name"]:
+        if "frame_kernel" not in r["Kernel_Name"] and "quad_kernel" not in r["Kernel_Name"]:
             continue
         c = r["Counter_Name"]
         tot[c] = tot.get(c, 0.0) + float(r["Counter_Value"])
