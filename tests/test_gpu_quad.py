@@ -23,13 +23,25 @@ def test_quad_chain_mixed_whole_piece_frames(vp8g):
     assert not bad, f"{len(bad)} slots differ, e.g. {bad[:8]}"
 
 
-def test_quad_chain_mirror_split_forced(vp8g):
-    """The same kind of batch with the mirror split forced (VP8G_SPLITCHAIN=1, child process): a
+def test_quad_chain_cut_and_unaligned_pieces(vp8g):
+    """Widths that are not multiples of 16 (1, 8, 15, 17, 33, 52, 100, 250, 1000) mixed with
+    whole-piece frames: the right MB's row pieces are cut and rows start unaligned (stride = width),
+    so the batch takes the quad kernel's general instantiation (byte path for those pieces); every
+    slot equals the oracle's output, the empty slots stay untouched."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import quad_check
+    bad = quad_check.run(n=1200, seed=0x0DD5, sizes=quad_check.ODD_SIZES)
+    assert not bad, f"{len(bad)} slots differ, e.g. {bad[:8]}"
+
+
+@pytest.mark.parametrize("odd", [False, True])
+def test_quad_chain_mirror_split_forced(vp8g, odd):
+    """The same kinds of batch with the mirror split forced (VP8G_SPLITCHAIN=1, child process): a
     bottom segment's first quad reads the frame's context from device memory after the top
     segment's flag; two launches (the flags' epoch advances)."""
     env = dict(os.environ, VP8G_SPLITCHAIN="1")
-    r = subprocess.run([sys.executable, str(ROOT / "tests" / "quad_check.py")], capture_output=True, text=True, timeout=240,
-                       env=env)
+    r = subprocess.run([sys.executable, str(ROOT / "tests" / "quad_check.py")] + (["--odd"] if odd else []), capture_output=True,
+                       text=True, timeout=240, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout.strip().endswith("OK"), r.stdout
 
@@ -64,3 +76,35 @@ print(mode, "OK" if not bad and b.status_word() == 0 else f"BAD {bad[:8]} status
         assert r.stdout.strip().endswith("OK"), (env_extra, r.stdout)
         mode = int(r.stdout.split()[0])
         assert mode & vp8g.MODE_CHAIN and bool(mode & vp8g.MODE_QUAD) == (not env_extra), (env_extra, mode)
+
+
+def test_quad_chain_stalled_producer_ends_promptly(vp8g):
+    """A quad chain whose wave 1 never publishes its progress (libvp8g_stall.so: wait bound 20 ms):
+    the waits are bounded and sticky, so the launch ends promptly with the timeout bit in the status
+    word instead of hanging the chain (the quad's progress is published one step late, and its first
+    step's context load waits too -- every wait path bounded)."""
+    code = r"""
+import ctypes as C, sys, time
+sys.path.insert(0, sys.argv[1] + "/webp-decoder_amd")
+import torch, vp8g, vp8g_batch
+vp8g._libs["gpu"] = C.CDLL(sys.argv[1] + "/webp-decoder_amd/lib/diag/libvp8g_stall.so", use_errno=True)
+dev = torch.device("cuda:0")
+cus = torch.cuda.get_device_properties(0).multi_processor_count
+n = 2 * cus
+frames = [vp8g.synth_frame(160, 128, 0x5A11 ^ i, profile=i % 3) for i in range(8)]
+b = vp8g_batch.DeviceBatch(n, 160, 128, dev)
+for i in range(n):
+    b.fill(i, frames[i % 8], True)
+b.commit()
+stream = torch.cuda.current_stream(dev).cuda_stream
+t = time.time()
+b.launch(stream)
+torch.cuda.synchronize()
+print(b.status_word(), b.launch_mode(), round(time.time() - t, 3))
+"""
+    r = subprocess.run([sys.executable, "-c", code, str(ROOT)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    status, mode, secs = r.stdout.split()[-3:]
+    assert int(status) & 1, r.stdout  # VP8G_ERR_TIMEOUT (include/vp8g.h)
+    assert int(mode) & vp8g.MODE_QUAD, r.stdout
+    assert float(secs) < 10.0, r.stdout

@@ -3,7 +3,7 @@
 
 Compiles vp8g_kernels.hip with -DVP8G_MARKS (STAMP(i) -> an asm comment ";MARK_i"), then counts
 VALU / SALU / LDS / VMEM / branch instructions between consecutive markers of the chosen
-instantiation.  Usage: tools/section_counts.py [NW] [extra hipcc flags...]
+instantiation.  Usage: tools/section_counts.py [NW | quad | quadg] [extra hipcc flags...]
 """
 import collections, os, re, subprocess, sys, tempfile
 
@@ -19,7 +19,8 @@ lines = open(out).read().split("\n")
 sym = None
 for l in lines:
     # NW, or a mangled template-argument fragment such as 16ELb0ELb0ELb1 (the chain kernel)
-    m = re.match(r"^(_ZN\S*quad_kernelILi16\S*):\s*(;.*)?$", l) if nw == "quad" else re.match(r"^(_ZN\S*frame_kernelILi%s\S*):\s*(;.*)?$" % (nw if "E" in nw else nw + "ELb0ELb0ELb0"), l)
+    # quad: the whole-piece instantiation quad_kernel<16, true>; quadg: the general one
+    m = re.match(r"^(_ZN\S*quad_kernelILi16ELb%s\S*):\s*(;.*)?$" % ("1" if nw == "quad" else "0"), l) if nw.startswith("quad") else re.match(r"^(_ZN\S*frame_kernelILi%s\S*):\s*(;.*)?$" % (nw if "E" in nw else nw + "ELb0ELb0ELb0"), l)
     if m:
         sym = m.group(1)
         break

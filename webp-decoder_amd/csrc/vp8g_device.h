@@ -194,17 +194,20 @@ bool pick_chain_split(uint32_t n_frames, uint32_t ctx_cols, uint32_t workgroups,
 // slots in LDS and no mirror split (VP8G_CHAIN_IL=0 / 1 forces it off / on where it fits).
 bool pick_chain_interleave(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint32_t ctx_cols, uint32_t workgroups, bool split,
                            bool quad = false);
-// The quad chain kernel for this batch: every frame has whole 16-B / 8-B row pieces and is not
-// loop-filter-only (quad_supported), and VP8G_QUAD is not 0 (A/B experiments).  A quad launch needs
+// The quad chain kernel for this batch: no frame is loop-filter-only (quad_supported), and VP8G_QUAD
+// is not 0 (A/B experiments).  whole_pieces: every frame has whole, aligned 16-B / 8-B row pieces, so
+// launch_chain(..., whole = true) takes the kernel's lean instantiation (the general one adds a byte
+// path for pieces cut by the right edge or unaligned planes).  A quad launch needs
 // `snap` (every frame's context, n_frames * ctx_cols * kCtxBytesPerCol bytes) in every mode.
 bool quad_supported(const Vp8gFrameDesc* h_descs, uint32_t n_frames);
 bool pick_quad(const Vp8gFrameDesc* h_descs, uint32_t n_frames);
+bool whole_pieces(const Vp8gFrameDesc* h_descs, uint32_t n_frames);
 // split: `snap` holds n_frames * ctx_cols * kCtxBytesPerCol bytes, `flags` n_frames words that hold
 // no value equal to `epoch` (a per-launch counter) before the launch.
 hipError_t launch_chain(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const Vp8gBatchArrays& arrays, uint8_t* d_out,
                         uint32_t ctx_cols, hipStream_t stream, uint32_t workgroups, bool ordered, bool split = false,
                         uint8_t* snap = nullptr, uint32_t* flags = nullptr, uint32_t epoch = 0, bool interleave = false,
-                        bool quad = false);
+                        bool quad = false, bool whole = false);
 
 constexpr uint32_t kMaxSplit = 8;
 int device_cus();

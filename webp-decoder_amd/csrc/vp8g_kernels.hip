@@ -1950,13 +1950,20 @@ bool pick_chain_interleave(const Vp8gFrameDesc* h_descs, uint32_t n_frames, uint
 }
 
 bool quad_supported(const Vp8gFrameDesc* h_descs, uint32_t n_frames) {
-	// whole 16-B / 8-B row pieces (frame_kernel's fl_fast; the output base is at least 16-B aligned), no
-	// loop-filter-only frames
+	// every frame but loop-filter-only ones (frames without whole row pieces take the quad kernel's
+	// byte path at the right edge / for unaligned planes)
+	for (uint32_t i = 0; i < n_frames; i++)
+		if (h_descs[i].mb_cols != 0 && h_descs[i].mb_rows != 0 && (h_descs[i].flags & VP8G_F_LF_ONLY)) return false;
+	return true;
+}
+
+bool whole_pieces(const Vp8gFrameDesc* h_descs, uint32_t n_frames) {
+	// every 16-B luma / 8-B chroma row piece inside its frame and aligned (the output base is at least
+	// 16-B aligned): the quad kernel's lean instantiation
 	for (uint32_t i = 0; i < n_frames; i++) {
 		const Vp8gFrameDesc& d = h_descs[i];
 		if (d.mb_cols == 0 || d.mb_rows == 0) continue;
-		if ((d.flags & VP8G_F_LF_ONLY) || d.width != 16u * d.mb_cols || ((d.out_y | d.stride_y) & 15u) != 0 ||
-		    ((d.out_u | d.stride_uv | (d.out_v - d.out_u)) & 7u) != 0)
+		if (d.width != 16u * d.mb_cols || ((d.out_y | d.stride_y) & 15u) != 0 || ((d.out_u | d.stride_uv | (d.out_v - d.out_u)) & 7u) != 0)
 			return false;
 	}
 	return true;
@@ -1975,17 +1982,21 @@ bool pick_quad(const Vp8gFrameDesc* h_descs, uint32_t n_frames) {
 
 hipError_t launch_chain(const Vp8gFrameDesc* d_descs, uint32_t n_frames, const Vp8gBatchArrays& arrays, uint8_t* d_out,
                         uint32_t ctx_cols, hipStream_t stream, uint32_t workgroups, bool ordered, bool split, uint8_t* snap,
-                        uint32_t* flags, uint32_t epoch, bool interleave, bool quad) {
+                        uint32_t* flags, uint32_t epoch, bool interleave, bool quad, bool whole) {
 	if (n_frames == 0) return hipSuccess;
 	if ((split && (!snap || !flags)) || (kChainG && !snap) || (interleave && split)) return hipErrorInvalidValue;
 	const uint32_t list_max = (n_frames + workgroups - 1) / workgroups;
 	const size_t lds = chain_lds_bytes(ctx_cols, split ? 2 * list_max : list_max, n_frames, interleave, quad);
 	if (quad) {  // four MB rows per wave; the snapshot buffer holds every frame's context
 		if (!snap) return hipErrorInvalidValue;
-		static const hipError_t eq =
-		    hipFuncSetAttribute((const void*)quad_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLds);
-		if (eq != hipSuccess) return eq;
-		hipLaunchKernelGGL(quad_kernel<16>, dim3(workgroups), dim3(16 * 64), lds, stream, d_descs, arrays, d_out, ctx_cols, snap,
+		static const hipError_t eq1 =
+		    hipFuncSetAttribute((const void*)quad_kernel<16, true>, hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLds);
+		static const hipError_t eq0 =
+		    hipFuncSetAttribute((const void*)quad_kernel<16, false>, hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLds);
+		if (eq1 != hipSuccess) return eq1;
+		if (eq0 != hipSuccess) return eq0;
+		auto fq = whole ? quad_kernel<16, true> : quad_kernel<16, false>;
+		hipLaunchKernelGGL(fq, dim3(workgroups), dim3(16 * 64), lds, stream, d_descs, arrays, d_out, ctx_cols, snap,
 		                   split ? epoch : 1u, split ? flags : nullptr, (ordered ? 1u : 0u) | (split ? 2u : 0u) | (interleave ? 4u : 0u),
 		                   n_frames);
 		return hipGetLastError();

@@ -708,7 +708,8 @@ VP8G_API int vp8g_decode_webp_batch_ex(const ByteSpan* files, uint32_t n, int fi
 				const uint32_t wg = big || k > 1 || (vp8g::kChainG && !quad) ? 0u : vp8g::pick_chain(s.descs.data(), nf, max_cols, &ordered, quad);
 				if (wg)  // more frames than CUs: one 16-wave chain of frames per CU
 					PTRY(vp8g::launch_chain((const Vp8gFrameDesc*)(d + L.desc), nf, arr, d + L.out, max_cols, stream, wg, ordered, false,
-					                        quad ? d + L.gctx : nullptr, nullptr, 0u, false, quad),
+					                        quad ? d + L.gctx : nullptr, nullptr, 0u, false, quad,
+					                        quad && vp8g::whole_pieces(s.descs.data(), nf)),
 					     "recon launch");
 				else
 					PTRY(vp8g::launch_frames((const Vp8gFrameDesc*)(d + L.desc), nf, arr, d + L.out, max_cols, max_rows,
