@@ -51,7 +51,7 @@ if traces and bench_line:
     same = {
         "tag": tag,
         "source": "rocprofv3 --kernel-trace of the bench run whose line is in " + f"{tag}_trace_bench.json" +
-                  " (same process, same box); frame_kernel dispatches in launch order",
+                  " (same process, same box); bench-kernel (quad_kernel) dispatches in launch order",
         "dispatch_ms": [round(d, 3) for d in durs],
         "median_ms_excluding_first": round(med, 3),
         "bench_ms_per_step": bench_line["ms_per_step"],
@@ -82,7 +82,7 @@ write_b = write_kib * 1024
 mbs = 512 * 240 * 135
 out = {
     "frames": 512, "filtered": True, "width": 3840, "height": 2160,
-    "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, {n1}/{n2} dispatches of frame_kernel (the bench kernel), tag {tag}",
+    "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, {n1}/{n2} dispatches of the bench kernel (quad_kernel), tag {tag}",
     "fetch_size_kib_per_launch": round(fetch_kib, 1),
     "write_size_kib_per_launch": round(write_kib, 1),
     "hbm_read_bytes_per_launch": round(read_b),
@@ -90,10 +90,12 @@ out = {
     "hbm_bytes_per_launch": round(read_b + write_b),
     "per_mb": {"read": round(read_b / mbs, 1), "write": round(write_b / mbs, 1),
                "algorithmic_read": 820, "algorithmic_write": 384},
-    "note": "FETCH_SIZE doubled (gfx950 tallies 128-B requests at 64 B). Writes: the output row "
-            "pieces are 16 B (luma) / 8 B (chroma) per row per MB; with write-through (sc1) stores "
-            "(round 4) each counts as one 32-B write (16 x 32 + 16 x 32 = 1024 B per MB); with plain "
-            "stores (up to r04d) partially written lines were evicted and refilled from HBM",
+    "note": "FETCH_SIZE doubled (gfx950 tallies 128-B requests at 64 B). Writes: the quad kernel stores "
+            "each output row as pairs of MB columns (32 B luma / 16 B chroma per lane pair, write-through "
+            "sc1; a 16-B chroma pair still costs one 32-B write: 256 + 256 = 512 B per MB + the last "
+            "columns and the context entries). Before round 5's pairing: 16-B / 8-B pieces, one 32-B "
+            "write each with sc1 (1024 B per MB), or with plain stores partly written lines evicted and "
+            "refilled from HBM (1049 B written, 1637 B read per MB)",
 }
 (prof / "traffic_4k_batch.json").write_text(json.dumps(out, indent=1) + "\n")
 print(json.dumps(out, indent=1))
