@@ -108,3 +108,49 @@ print(b.status_word(), b.launch_mode(), round(time.time() - t, 3))
     assert int(status) & 1, r.stdout  # VP8G_ERR_TIMEOUT (include/vp8g.h)
     assert int(mode) & vp8g.MODE_QUAD, r.stdout
     assert float(secs) < 10.0, r.stdout
+
+
+def test_chain_output_base_not_16b_aligned(vp8g):
+    """The output base handed to vp8g_decode_batch_device 8 bytes past an aligned allocation, with
+    whole-piece descriptors (offsets and strides 16-B aligned): the quad chain must not take its
+    paired-store instantiation (which assumes a 16-B aligned base) -- and the pairs chain
+    (VP8G_QUAD=0) must be exact too; every slot equals the oracle's output and the 8 bytes before
+    the base stay untouched."""
+    code = r"""
+import ctypes as C, sys
+sys.path.insert(0, sys.argv[1] + "/webp-decoder_amd")
+import numpy as np, torch, vp8g, vp8g_batch
+dev = torch.device("cuda:0")
+n = 2 * torch.cuda.get_device_properties(0).multi_processor_count
+frames = [vp8g.synth_frame(160, 64, 0xA11 ^ i, profile=i % 3) for i in range(8)]
+b = vp8g_batch.DeviceBatch(n, 160, 64, dev)
+for i in range(n):
+    b.fill(i, frames[i % 8], i % 3 != 0)
+b.commit()
+big = torch.full((n * b.frame_bytes + 64,), 0xA5, dtype=torch.uint8, device=dev)
+lib = vp8g.gpu_lib()
+stream = torch.cuda.current_stream(dev).cuda_stream
+rc = lib.vp8g_decode_batch_device(b.h_descs, C.c_void_p(b.d_descs.data_ptr()), n, C.byref(b.c_arrays),
+                                  C.c_void_p(big.data_ptr() + 8), C.c_void_p(stream), 0)
+assert rc == 0, lib.vp8g_last_error()
+torch.cuda.synchronize()
+host = big.cpu().numpy()
+exp, bad = {}, []
+for i in range(n):
+    key = (i % 8, i % 3 != 0)
+    if key not in exp:
+        exp[key] = vp8g.oracle_reconstruct(frames[i % 8], key[1])
+    o = 8 + i * b.frame_bytes
+    if host[o:o + len(exp[key])].tobytes() != exp[key]:
+        bad.append(i)
+if host[:8].tobytes() != b"\xa5" * 8:
+    bad.append("bytes before the base written")
+print(b.launch_mode(), "OK" if not bad and b.status_word() == 0 else f"BAD {bad[:8]} status {b.status_word()}")
+"""
+    for env_extra in ({}, {"VP8G_QUAD": "0"}):
+        env = dict(os.environ, **env_extra)
+        r = subprocess.run([sys.executable, "-c", code, str(ROOT)], capture_output=True, text=True, timeout=240, env=env)
+        assert r.returncode == 0, (env_extra, r.stderr[-2000:])
+        assert r.stdout.strip().endswith("OK"), (env_extra, r.stdout)
+        mode = int(r.stdout.split()[-2])
+        assert mode & vp8g.MODE_CHAIN and bool(mode & vp8g.MODE_QUAD) == (not env_extra), (env_extra, mode)

@@ -429,7 +429,7 @@ int run_locked(DevState& g_dev, const std::vector<Vp8gFrameDesc>& descs, const V
 		g_mode = VP8G_MODE_CHAIN | (split ? VP8G_MODE_MIRROR_SPLIT : 0u) | (il ? VP8G_MODE_INTERLEAVE : 0u) | (quad ? VP8G_MODE_QUAD : 0u);
 		HIP_TRY(vp8g::launch_chain((const Vp8gFrameDesc*)d_descs, n, arr, d_out, max_cols, s, wg, ordered, split, g_dev.snap,
 		                           (uint32_t*)g_dev.sflags, g_dev.epoch, il, quad,
-		                           quad && vp8g::whole_pieces(descs.data(), n)),
+		                           quad && vp8g::whole_pieces(descs.data(), n) && ((uintptr_t)d_out & 15u) == 0),
 		        "launch");
 	} else {
 		const uint32_t ord = vp8g::pick_order(descs.data(), n, 1);  // cost-balanced placement (vp8g_device.h)
