@@ -1069,8 +1069,8 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 			fl_offC = (pc ? vofs : 0u) + __umul24(prowC, suv);
 			const bool nlast = rr + 1 < R;
 			fl_bits = (row_ok && ln < 20 && prowY < H ? 1u : 0u) | (ln >= 16 && nlast ? 2u : 0u) |
-			          (((yal + fl_offY) & 3u) == 0 ? 4u : 0u) | (row_ok && ln < 24 && prowC < CH ? 8u : 0u) |
-			          (kc >= 8 && nlast ? 16u : 0u) | (((ual + fl_offC) & 3u) == 0 ? 32u : 0u);
+			          4u | (row_ok && ln < 24 && prowC < CH ? 8u : 0u) |
+			          (kc >= 8 && nlast ? 16u : 0u) | 32u;
 			// Whole-piece frames (fl_fast): every row piece of a column inside the frame is a full,
 			// aligned 16-B / 8-B store.  The offsets then fold the lane's column shift (the left MB for
 			// tile rows >= 4) in, and a lane that never stores to HBM this pair (outside the crop, or
@@ -1572,7 +1572,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 				const uint32_t colpx = col * 16u;
 				const uint32_t off = __umul24(prow, sy) + colpx;
 				const bool vis = ok && prow < H && !(VP8G_ABLATE & 4);
-				const bool full = colpx + 16u <= W && ((yal + off) & 3u) == 0;
+				const bool full = colpx + 16u <= W;
 				bst128(rY, vis && full ? off : kNoStore, u32x4{lo.x, lo.y, hi.x, hi.y});
 				if (__ballot(vis && !full) != 0ull) {
 					if (vis && !full) {
@@ -1585,7 +1585,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 				const uint32_t colpx = col * 8u;
 				const uint32_t off = (p ? vofs : 0u) + __umul24(prow, suv) + colpx;  // from outU
 				const bool vis = ok && prow < CH && !(VP8G_ABLATE & 4);
-				const bool full = colpx + 8u <= CW && ((ual + off) & 3u) == 0;
+				const bool full = colpx + 8u <= CW;
 				bst64(rC, vis && full ? off : kNoStore, lo);
 				if (__ballot(vis && !full) != 0ull) {
 					if (vis && !full) {
@@ -1613,7 +1613,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					const uint32_t colpx = cu * 16u, prow = y0 + (uint32_t)(ln & 15);
 					const uint32_t off = __umul24(prow, sy) + colpx;
 					const bool vis = act && yl && prow < H && !(VP8G_ABLATE & 4);
-					const bool full = colpx + 16u <= W && ((yal + off) & 3u) == 0;
+					const bool full = colpx + 16u <= W;
 					offY = vis && full ? off : kNoStore;
 					poffY = off, pcntY = vis && !full ? min(W - colpx, 16u) : 0u;
 				}
@@ -1621,7 +1621,7 @@ __global__ __launch_bounds__(NW * 64, min_waves_per_simd<NW>()) void frame_kerne
 					const uint32_t colpx = cu * 8u, prow = cy0 + (uint32_t)row;
 					const uint32_t off = (p ? vofs : 0u) + __umul24(prow, suv) + colpx;
 					const bool vis = act && !yl && prow < CH && !(VP8G_ABLATE & 4);
-					const bool full = colpx + 8u <= CW && ((ual + off) & 3u) == 0;
+					const bool full = colpx + 8u <= CW;
 					offC = vis && full ? off : kNoStore;
 					poffC = off, pcntC = vis && !full ? min(CW - colpx, 8u) : 0u;
 				}
