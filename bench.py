@@ -621,8 +621,8 @@ def main(argv=None):
             "parity": head["parity"],
             "kernel_ms_per_step": head["kernel_ms_per_step"],
             "kernel_ms_steps": head["kernel_ms_steps"],
-            "roofline": dict(head["roofline"], binding_resource=("latency-bound issue at 4 waves per SIMD (quad chain kernel: 502 instructions / 336 VALU per MB, "
-                                                               "~1.2 per quad-cycle per SIMD); HBM traffic 1.28x algorithmic after the paired "
+            "roofline": dict(head["roofline"], binding_resource=("latency-bound issue at 4 waves per SIMD (quad chain kernel: ~499 instructions / 332 VALU per MB, "
+                                                               "~1.2 per quad-cycle per SIMD); HBM traffic 1.29x algorithmic after the paired "
                                                                "write-through stores; DESIGN.md §3.1, §5")),
             "cpu_baseline": head["cpu_baseline"],
         }
