@@ -69,7 +69,36 @@ WORKLOADS = {
 FIXTURES = UHD  # (back-compat name used by tools/)
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 E2E_REPS = 3  # end-to-end legs: median of this many calls (host page-cache and allocator state vary call to call)
-TRAFFIC_FILE = ROOT / "profiles" / "traffic_4k_batch.json"
+# measured HBM traffic per launch (rocprofv3 PMC passes, tools/profile_round.sh + traffic_summary.py)
+TRAFFIC_FILES = {"uhd4": ROOT / "profiles" / "traffic_4k_batch.json", "synth": ROOT / "profiles" / "traffic_synth_batch.json"}
+TRAFFIC_FILE = TRAFFIC_FILES["uhd4"]
+# the committed PMC summary of the shipped kernel on uhd4 (tools/pmc_pass.sh + pmc_json.py): the
+# instruction mix quoted in roofline.binding_resource comes from it, not from this run
+PMC_FILE = ROOT / "profiles" / "r05f_quad_kernel_pmc.json"
+
+
+def binding_resource() -> str:
+    """What limits the kernel, from the committed profiles (not from this run): the PMC instruction mix
+    (PMC_FILE) and the HBM traffic ratio (TRAFFIC_FILE), each named with its source."""
+    parts = ["latency-bound issue at 4 waves per SIMD (quad chain kernel)"]
+    try:
+        pj = json.loads(PMC_FILE.read_text())
+        pm = pj["per_mb"]
+        tot = pm["valu"] + pm["salu"] + pm["lds"] + pm["branch"] + pm["vmem_rd"] + pm["vmem_wr"]
+        shares = pj.get("wave_time_shares", {})
+        parts.append(f"{tot:.0f} instructions / {pm['valu']:.0f} VALU per MB, wave time {100 * shares.get('active_inst_any', 0):.0f} % "
+                     f"issuing / {100 * shares.get('wait_inst_any', 0):.0f} % waiting on a result ({PMC_FILE.name})")
+    except (OSError, KeyError, ValueError):
+        pass
+    try:
+        tj = json.loads(TRAFFIC_FILE.read_text())
+        pm = tj["per_mb"]
+        ratio = (pm["read"] + pm["write"]) / (pm["algorithmic_read"] + pm["algorithmic_write"])
+        parts.append(f"HBM traffic {ratio:.2f}x algorithmic read + write ({TRAFFIC_FILE.name}; FETCH_SIZE counted x2, "
+                     "the gfx950 correction calibrated by tools/ubench/fetch_calib.hip, DESIGN.md §5)")
+    except (OSError, KeyError, ValueError, ZeroDivisionError):
+        pass
+    return "; ".join(parts) + "; DESIGN.md §3.1, §5"
 
 
 def parse(argv=None):
@@ -382,10 +411,12 @@ def run_workload(name, args, rank, world, dist, dev, golden, rank_factory=Rank):
                  "whole_block_prediction", "b_pred", "save_ctx", "loopfilter", "store", "publish"]
         obj["stamps"] = {k: round(acc[i] / tot, 4) for i, k in zip(slots, names)}
         obj["stamps"]["cycles_per_mb_per_wave"] = round(tot / (r.batch.total_mb * args.steps), 1)
-    if name == "uhd4" and TRAFFIC_FILE.exists():
-        tj = json.loads(TRAFFIC_FILE.read_text())
-        if tj.get("frames") == r.n and tj.get("filtered") == r.filtered:
+    tf = TRAFFIC_FILES.get(name)
+    if tf is not None and tf.exists():
+        tj = json.loads(tf.read_text())
+        if tj.get("frames") == r.n and tj.get("filtered") == r.filtered and tj.get("workload", "uhd4") == name:
             obj["roofline"]["traffic"] = tj.get("hbm_bytes_per_launch")
+            obj["roofline"]["traffic_source"] = f"{tf.relative_to(ROOT)} ({tj.get('tag', tj.get('source', ''))})"
     if rank == 0 and world == 1 and not args.no_cpu_baseline and r.cpu_frames:
         secs = args.cpu_seconds if name == args.workload else args.cpu_seconds / 2
         obj["cpu_baseline"] = cpu_baseline(r.cpu_frames, r.filtered, args.cpu_threads or all_cores(), secs,
@@ -621,9 +652,7 @@ def main(argv=None):
             "parity": head["parity"],
             "kernel_ms_per_step": head["kernel_ms_per_step"],
             "kernel_ms_steps": head["kernel_ms_steps"],
-            "roofline": dict(head["roofline"], binding_resource=("latency-bound issue at 4 waves per SIMD (quad chain kernel: ~499 instructions / 332 VALU per MB, "
-                                                               "~1.2 per quad-cycle per SIMD); HBM traffic 1.29x algorithmic after the paired "
-                                                               "write-through stores; DESIGN.md §3.1, §5")),
+            "roofline": dict(head["roofline"], binding_resource=binding_resource()),
             "cpu_baseline": head["cpu_baseline"],
         }
         if extra:

@@ -352,8 +352,10 @@ int vp8g_encode_batch_device(const Vp8gEncDesc* h_descs, const Vp8gEncDesc* d_de
 /* Name of the last HIP error seen by this library in the calling thread ("" if none). */
 const char* vp8g_last_error(void);
 
-/* How the calling thread's last reconstruction launch (vp8g_decode_batch_device, the host entry
- * points) ran: VP8G_MODE_* bits, 0 = one workgroup per frame.  Diagnostics and tests. */
+/* How the calling thread's last reconstruction launch through vp8g_decode_batch_device or the
+ * reference entry points ran: VP8G_MODE_* bits, 0 = one workgroup per frame (also after a call that
+ * failed before its launch).  The end-to-end batch path (vp8g_decode_webp_batch[_ex]) does not set
+ * it.  Diagnostics and tests. */
 #define VP8G_MODE_CHAIN 1u        /* one 16-wave workgroup per CU decodes a chain of frames */
 #define VP8G_MODE_MIRROR_SPLIT 2u /* frames split between a workgroup and its mirror */
 #define VP8G_MODE_INTERLEAVE 4u   /* two frames of a chain interleaved */

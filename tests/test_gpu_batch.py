@@ -238,8 +238,13 @@ def test_device_batch_512_uhd_bench_launch(vp8g, digests):
     0's shard of BASELINE configs[3] / [4]): the chain kernel with the mirror split, every slot."""
     b, bad = run_batch(vp8g, UHD, 512, True, digests, slot0=0)
     assert not bad, f"{len(bad)} of 512 slots differ, e.g. {bad[:8]}"
-    mode = b.launch_mode()  # (the quad chain with the mirror split, as bench.py's launch)
-    assert mode & vp8g.MODE_CHAIN and mode & vp8g.MODE_QUAD and mode & vp8g.MODE_MIRROR_SPLIT, mode
+    mode = b.launch_mode()  # (the quad chain, as bench.py's launch)
+    assert mode & vp8g.MODE_CHAIN and mode & vp8g.MODE_QUAD, mode
+    # (the mirror split needs at most two frames per workgroup: 512 frames on >= 256 CUs, as on
+    # MI355X; a part with fewer CUs decodes the same batch without it -- ADVICE r05)
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    if -(-512 // cus) <= 2:
+        assert mode & vp8g.MODE_MIRROR_SPLIT, mode
     del b
     torch.cuda.empty_cache()
 

@@ -75,14 +75,17 @@ print(mode, "OK" if not bad and b.status_word() == 0 else f"BAD {bad[:8]} status
         assert r.returncode == 0, (env_extra, r.stderr[-2000:])
         assert r.stdout.strip().endswith("OK"), (env_extra, r.stdout)
         mode = int(r.stdout.split()[0])
-        assert mode & vp8g.MODE_CHAIN and bool(mode & vp8g.MODE_QUAD) == (not env_extra), (env_extra, mode)
+        quad = env_extra.get("VP8G_QUAD") != "0"
+        assert mode & vp8g.MODE_CHAIN and bool(mode & vp8g.MODE_QUAD) == quad, (env_extra, mode)
 
 
 def test_quad_chain_stalled_producer_ends_promptly(vp8g):
     """A quad chain whose wave 1 never publishes its progress (libvp8g_stall.so: wait bound 20 ms):
     the waits are bounded and sticky, so the launch ends promptly with the timeout bit in the status
     word instead of hanging the chain (the quad's progress is published one step late, and its first
-    step's context load waits too -- every wait path bounded)."""
+    step's context load waits too -- every wait path bounded).  Frames of 128 MB rows: 16 quads per
+    mirror-split segment, so wave 1's units have successors that wait on its progress whatever the
+    schedule."""
     code = r"""
 import ctypes as C, sys, time
 sys.path.insert(0, sys.argv[1] + "/webp-decoder_amd")
@@ -91,8 +94,8 @@ vp8g._libs["gpu"] = C.CDLL(sys.argv[1] + "/webp-decoder_amd/lib/diag/libvp8g_sta
 dev = torch.device("cuda:0")
 cus = torch.cuda.get_device_properties(0).multi_processor_count
 n = 2 * cus
-frames = [vp8g.synth_frame(160, 128, 0x5A11 ^ i, profile=i % 3) for i in range(8)]
-b = vp8g_batch.DeviceBatch(n, 160, 128, dev)
+frames = [vp8g.synth_frame(160, 2048, 0x5A11 ^ i, profile=i % 3) for i in range(8)]
+b = vp8g_batch.DeviceBatch(n, 160, 2048, dev)
 for i in range(n):
     b.fill(i, frames[i % 8], True)
 b.commit()

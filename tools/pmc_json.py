@@ -1,11 +1,13 @@
 #!/usr/bin/env python3
 """Per-MB instruction / wait / LDS summary of a tools/pmc_pass.sh run of the bench kernel, as the
 committed profiles/<tag>_<kernel>_pmc.json (default kernel: quad_kernel, the bench's chain) (DESIGN.md §5 takes its numbers from it).
-  tools/pmc_json.py <pmc dir> <tag> <build> [kernel filter]"""
+  tools/pmc_json.py <pmc dir> <tag> <build> [kernel filter] [workload: uhd4 | synth]"""
 import collections, csv, glob, json, pathlib, sys
 
 d, tag, build = sys.argv[1], sys.argv[2], sys.argv[3]
 filt = sys.argv[4] if len(sys.argv) > 4 else "quad_kernel"
+wl = sys.argv[5] if len(sys.argv) > 5 else "uhd4"
+WL_TEXT = {"uhd4": "uhd4: 512 x 3840x2160, -yuvf", "synth": "synth: 512 x 3840x2160 distinct vp8_synth profile-0 frames, -yuvf"}
 c = {}
 kname = None
 for f in sorted(glob.glob(d + "/pmc*/pmc_counter_collection.csv")):
@@ -23,7 +25,7 @@ per_mb = {k[9:].lower() if k.startswith("SQ_INSTS_") else k.lower(): round(c[k] 
 out = {
     "kernel": kname.split("(")[0] if kname else filt,
     "build": build,
-    "workload": "uhd4: 512 x 3840x2160, -yuvf",
+    "workload": WL_TEXT[wl],
     "source": "rocprofv3 --pmc, one counter group per run (tools/pmc_pass.sh), last dispatch; gpurun_out/" + pathlib.Path(d).name,
     "counters": c,
     "per_mb": per_mb,

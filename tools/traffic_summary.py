@@ -1,11 +1,12 @@
 #!/usr/bin/env python3
 """Turn a tools/profile_round.sh run into the committed profile files.
 
-  tools/traffic_summary.py <tag>   (reads gpurun_out/prof_<tag>/, writes profiles/)
+  tools/traffic_summary.py <tag> [workload]   (reads gpurun_out/prof_<tag>/, writes profiles/;
+                                               workload uhd4 (default) or synth)
 
 * profiles/<tag>_kernel_stats.csv   -- rocprofv3 --stats summary of the bench command
 * profiles/<tag>_trace_bench.json   -- the bench line printed under the profiler
-* profiles/traffic_4k_batch.json    -- HBM bytes per launch of the bench kernel from the PMC
+* profiles/traffic_4k_batch.json    -- (uhd4; synth: traffic_synth_batch.json) HBM bytes per launch of the bench kernel from the PMC
   passes: FETCH_SIZE (KiB; x2 on gfx950 for wide coalesced reads, MI355X_MICROARCH.md "HBM")
   + WRITE_SIZE (KiB), averaged over the frame_kernel dispatches.  bench.py reports it as
   roofline.traffic.
@@ -20,6 +21,8 @@ import sys
 
 ROOT = pathlib.Path(__file__).resolve().parent.parent
 tag = sys.argv[1]
+workload = sys.argv[2] if len(sys.argv) > 2 else "uhd4"
+assert workload in ("uhd4", "synth"), workload
 src = ROOT / "gpurun_out" / f"prof_{tag}"
 prof = ROOT / "profiles"
 prof.mkdir(exist_ok=True)
@@ -81,7 +84,7 @@ read_b = fetch_kib * 1024 * 2
 write_b = write_kib * 1024
 mbs = 512 * 240 * 135
 out = {
-    "frames": 512, "filtered": True, "width": 3840, "height": 2160,
+    "workload": workload, "tag": tag, "frames": 512, "filtered": True, "width": 3840, "height": 2160,
     "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, {n1}/{n2} dispatches of the bench kernel (quad_kernel), tag {tag}",
     "fetch_size_kib_per_launch": round(fetch_kib, 1),
     "write_size_kib_per_launch": round(write_kib, 1),
@@ -97,5 +100,5 @@ out = {
             "write each with sc1 (1024 B per MB), or with plain stores partly written lines evicted and "
             "refilled from HBM (1049 B written, 1637 B read per MB)",
 }
-(prof / "traffic_4k_batch.json").write_text(json.dumps(out, indent=1) + "\n")
+(prof / ("traffic_4k_batch.json" if workload == "uhd4" else "traffic_synth_batch.json")).write_text(json.dumps(out, indent=1) + "\n")
 print(json.dumps(out, indent=1))

@@ -190,7 +190,7 @@ std::atomic<size_t> g_held{0};
 
 vp8g::GateScope::GateScope(hipStream_t s) : s_(s) {
 	g_gate.mu.lock();
-	const hipError_t before = hipPeekAtLastError();  // (a caller's pending error stays for the caller)
+	const hipError_t before = hipPeekAtLastError();
 	if (g_gate.xpending) {
 		const hipError_t q = hipEventQuery(g_gate.xev);
 		if (q == hipSuccess) g_gate.xpending = false;
@@ -202,8 +202,10 @@ vp8g::GateScope::GateScope(hipStream_t s) : s_(s) {
 		if (hipEventQuery(x.ev) == hipSuccess) x.live = false;
 		else may_cross_ = false;  // in flight (or unknown): no cross-workgroup launch beside it
 	}
-	// (hipErrorNotReady of the queries must not read as a launch failure later; an error that was
-	// pending before them is left alone)
+	// (hipErrorNotReady of the queries must not read as a launch failure later, so it is cleared.  HIP
+	// keeps one last-error slot per thread: a caller's error pending before the gate stays pending
+	// only when no query replaced it; after a query that returned hipErrorNotReady it is already gone,
+	// and clearing the slot then loses nothing more)
 	if (before == hipSuccess || hipPeekAtLastError() == hipErrorNotReady) (void)hipGetLastError();
 }
 
@@ -357,6 +359,7 @@ int run_locked(DevState& g_dev, const std::vector<Vp8gFrameDesc>& descs, const V
 		if (d.mb_rows > max_rows) max_rows = d.mb_rows;
 	}
 	const uint32_t n = (uint32_t)descs.size();
+	g_mode = 0u;  // (a call that fails before its launch reports no mode, not the previous call's)
 	if (g_dev.pending) {  // the previous (asynchronous) launch on this context's buffers comes first
 		HIP_TRY(hipStreamWaitEvent(s, g_dev.done, 0), "hipStreamWaitEvent");
 	}

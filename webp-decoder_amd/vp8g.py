@@ -248,7 +248,8 @@ def gpu_lib():
         lib.vp8g_reconstruct_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int, P(Yuv420Image)]
         lib.vp8g_last_error.restype = C.c_char_p
         lib.vp8g_abi_version.restype = C.c_uint32
-        lib.vp8g_last_launch_mode.restype = C.c_uint32
+        if hasattr(lib, "vp8g_last_launch_mode"):  # (libraries built before round 5 lack it: A/B of old builds)
+            lib.vp8g_last_launch_mode.restype = C.c_uint32
         lib.yuv420_write_ppm_fd.argtypes = [C.c_int, P(Yuv420Image)]
         lib.yuv420_write_png_fd.argtypes = [C.c_int, P(Yuv420Image)]
         lib.vp8g_encoded_size.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32]

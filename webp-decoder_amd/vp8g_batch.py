@@ -117,8 +117,12 @@ class DeviceBatch:
         return self.digest_buf.cpu().numpy().view(np.uint64).copy()
 
     def launch_mode(self) -> int:
-        """VP8G_MODE_* bits of this thread's last launch (include/vp8g.h vp8g_last_launch_mode)."""
-        return int(vp8g.gpu_lib().vp8g_last_launch_mode())
+        """VP8G_MODE_* bits of this thread's last launch (include/vp8g.h vp8g_last_launch_mode); -1 when
+        the loaded library predates the symbol (an older build under VP8G_LIB)."""
+        lib = vp8g.gpu_lib()
+        if not hasattr(lib, "vp8g_last_launch_mode"):
+            return -1
+        return int(lib.vp8g_last_launch_mode())
 
     def status_word(self) -> int:
         return int(self.status[0].item())
