@@ -117,7 +117,10 @@ constexpr int kChainWgPerCu = VP8G_CHAIN_WPC;
 // quarter areas (the half layout without the iWHT scratch) and four 3-column context rings; the
 // context between waves lives in device memory (the snapshot buffer, one region per frame), so the
 // quad chain's LDS does not depend on the frame width.  Chosen per batch (pick_quad).
-constexpr int kQuarterBytes = kWht;                          // tile, borders, B_PRED buffers, residual park
+#ifndef VP8G_QPAD  // (experiment: quarter stride padding; 4 puts quarters 1 and 3 on the odd LDS banks)
+#define VP8G_QPAD 0
+#endif
+constexpr int kQuarterBytes = kWht + VP8G_QPAD;              // tile, borders, B_PRED buffers, residual park
 constexpr int kRingBytes = 3 * kCtxBytesPerCol;              // three MB columns of context
 constexpr int kQRings = kHdrBytes + 4 * kQuarterBytes;       // wave-relative: ring h at + h * kRingBytes
 constexpr int kQWaveBytes = 4 * kQuarterBytes + 4 * kRingBytes;
