@@ -50,7 +50,7 @@ oracle:
 # Diagnostic variants of libvp8g (never loaded by the product path; select with VP8G_LIB=...):
 # per-phase shader-clock stamps, and phase ablations (timing only, wrong output).
 DIAG := $(LIB)/diag
-DIAG_VARIANTS := stamps abl1 abl2 abl4 abl8 abl15 abl16 abl32 pairs
+DIAG_VARIANTS := stamps abl1 abl2 abl4 abl8 abl15 abl16 abl32 abl47 pairs
 diag: $(foreach v,$(DIAG_VARIANTS),$(DIAG)/libvp8g_$(v).so) $(DIAG)/libvp8g_stall.so
 $(DIAG):
 	mkdir -p $@
