@@ -74,7 +74,7 @@ TRAFFIC_FILES = {"uhd4": ROOT / "profiles" / "traffic_4k_batch.json", "synth": R
 TRAFFIC_FILE = TRAFFIC_FILES["uhd4"]
 # the committed PMC summary of the shipped kernel on uhd4 (tools/pmc_pass.sh + pmc_json.py): the
 # instruction mix quoted in roofline.binding_resource comes from it, not from this run
-PMC_FILE = ROOT / "profiles" / "r06zz_quad_kernel_pmc.json"
+PMC_FILE = ROOT / "profiles" / "r06fin_quad_kernel_pmc.json"
 
 
 def binding_resource() -> str:
